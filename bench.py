@@ -1,0 +1,270 @@
+"""bench.py -- bigblob write path, device-resident, GiB/s hashed.
+
+Workload (BASELINE.json metric, configs[2] / configs[4]): a synthetic blob of
+--size-gib GiB per GPU (default 64) at 1 MiB blocks, resident in HBM before
+the timed region.  One step = the whole bigblob write of that blob on the GPU
+(bigblob/blob.go:85-206 closed form): every data block posted (DEK = keyed
+BLAKE3, ChaCha20 ctext written to HBM, CID = BLAKE3 of ctext), the index
+nodes above them, and the root.  With N GPUs each rank owns a contiguous,
+bf-aligned block range of an N x size blob (weak scaling, no data-path
+collective); the level-1 refs (64 B per 16 GiB) are gathered once per step
+and rank 0 builds the root.
+
+Prints ONE JSON line (rank 0).  Extra objects: roofline (dominant kernel,
+HIP events on the launch stream), cpu_baseline (the oracle on host cores),
+host_round_trip (host memory -> GPU -> host ctext + refs), valu (second
+roofline).  Data is synthetic: splitmix64 stream (oracle_fill_splitmix).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB, MIB = 1 << 30, 1 << 20
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz
+# int-VALU ops per plaintext byte (DESIGN.md "Rooflines"): BLAKE3 compression
+# ~700 ops / 64 B (x 1.06 for parents), ChaCha20 block ~1010 ops / 64 B.
+OPS_PER_BYTE = {"dek": 700 * 1.06 / 64, "cid": (1010 + 700 * 1.06) / 64}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--size-gib", type=float, default=64.0, help="blob bytes per GPU")
+    p.add_argument("--block-size", type=int, default=MIB)
+    p.add_argument("--seed", type=int, default=3)
+    p.add_argument("--no-ctext", action="store_true",
+                   help="do not write ctext (NOT the headline configuration)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip roofline/cpu/host legs (profiling runs)")
+    p.add_argument("--cpu-sample-mib", type=int, default=1024)
+    p.add_argument("--host-rt-gib", type=float, default=4.0)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from glfs_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    N.set_device(local if world > 1 else 0)
+
+    bs = args.block_size
+    bf = bs // 64
+    per = int(args.size_gib * GIB) // bs * bs      # bytes per rank, whole blocks
+    nb = per // bs
+    assert nb % bf == 0 or world == 1, "per-rank range must be bf-aligned"
+    total = per * world
+    n0 = total // bs
+    first = rank * nb
+
+    stream = torch.cuda.Stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    with torch.cuda.stream(stream):
+        data = torch.empty(per, dtype=torch.uint8, device="cuda")
+        ctext = None if args.no_ctext else torch.empty(per, dtype=torch.uint8, device="cuda")
+        N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), first * bs, per,
+                                                  args.seed, sp))
+    stream.synchronize()
+    ct_ptr = None if ctext is None else ctext.data_ptr()
+
+    root = N.glfsx_root()
+    n_posts = ctypes.c_uint64()
+    lvl1 = ctypes.create_string_buffer(64 * max(1, -(-nb // bf)))
+
+    def step():
+        if world == 1:
+            N.check(N.lib.glfsx_create_device(bs, None, None, data.data_ptr(), per, ct_ptr,
+                                              ctypes.byref(root), ctypes.byref(n_posts), sp))
+            return
+        N.check(N.lib.glfsx_shard_device(bs, None, None, data.data_ptr(), total, first, nb,
+                                         ct_ptr, lvl1, sp))
+        m = -(-nb // bf)
+        mine = torch.frombuffer(bytearray(lvl1.raw[:64 * m]), dtype=torch.uint8).cuda()
+        gathered = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)  # 256 B per rank: the only exchange
+        if rank == 0:
+            allrefs = b"".join(bytes(g.cpu().numpy().tobytes()) for g in gathered)
+            N.check(N.lib.glfsx_root_from_level1(bs, None, None, allrefs,
+                                                 len(allrefs) // 64, total,
+                                                 ctypes.byref(root)))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    gibs = total / GIB * args.steps / dt
+
+    out = {
+        "metric": "GiB/s hashed, device-resident 1 MiB chunks, bigblob write; 1/2/4/8 MI355X",
+        "value": round(gibs, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (splitmix64 byte stream, generated in HBM)",
+        "config": {"workload": f"bigblob write {args.size_gib:g} GiB/GPU @ {bs // 1024} KiB "
+                               f"blocks, device-resident, ctext {'off' if ctext is None else 'to HBM'}",
+                   "blob_bytes": total, "block_size": bs, "blocks": n0,
+                   "posts_per_step": n_posts.value if world == 1 else None,
+                   "parallelism": f"disjoint block ranges x{world}"},
+        "root_cid": bytes(root.ref[:32]).hex() if rank == 0 else None,
+    }
+
+    if rank == 0 and not args.no_extras:
+        out["roofline"], out["valu"] = roofline(torch, N, data, ctext, per, bs, stream, sp)
+        out["cpu_baseline"] = cpu_baseline(args)
+        out["host_round_trip"] = host_round_trip(N, args, bs)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
+    """Per-kernel average duration with HIP events on the launch stream: the
+    DEK pass (reads ptext) and the ChaCha20+CID pass (reads ptext, writes
+    ctext).  achieved = algorithmic bytes per launch / avg duration."""
+    nblk = per // bs
+    refs = torch.zeros(64 * nblk, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    salt = bytes(32)
+    ct = None if ctext is None else ctext.data_ptr()
+    times = {"dek": [], "cid": []}
+    with torch.cuda.stream(stream):
+        for _ in range(reps + 1):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(stream)
+            N.check(N.lib.glfsx_dek_batch_device(salt, data.data_ptr(), per, bs,
+                                                 refs.data_ptr(), sp))
+            e[1].record(stream)
+            N.check(N.lib.glfsx_cid_batch_device(data.data_ptr(), per, bs, ct,
+                                                 refs.data_ptr(), None, sp))
+            e[2].record(stream)
+            e[2].synchronize()
+            times["dek"].append(e[0].elapsed_time(e[1]))
+            times["cid"].append(e[1].elapsed_time(e[2]))
+    avg = {k: sum(v[1:]) / reps for k, v in times.items()}  # first rep = warm-up
+    alg = {"dek": per, "cid": per * (2 if ct is not None else 1)}
+    dom = max(avg, key=avg.get)
+    achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": {"dek": "k_pass<4,false,true> (keyed BLAKE3, DEK)",
+                       "cid": "k_pass<4,true,true> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
+            "algorithmic_bytes_per_launch": alg[dom],
+            "avg_ms": {k: round(v, 4) for k, v in avg.items()},
+            "hashed_GBps": {k: round(per / (v * 1e-3) / 1e9, 1) for k, v in avg.items()}}
+    ops = {k: OPS_PER_BYTE[k] * per for k in avg}
+    valu = {"bound": "valu", "unit": "Tops/s", "peak": round(VALU_PEAK_TOPS, 2),
+            "ops_per_byte": {k: round(v, 2) for k, v in OPS_PER_BYTE.items()},
+            "achieved": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12, 2) for k in avg},
+            "frac": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 3)
+                     for k in avg}}
+    del refs
+    return roof, valu
+
+
+def cpu_baseline(args):
+    """The oracle (a C restatement of the same per-block sequence: keyed
+    BLAKE3, ChaCha20, BLAKE3 CID, ctext into a buffer) timed on host cores over
+    a bounded sample of the same workload (1 MiB blocks of the same stream)."""
+    from oracle import oracle as O
+    L = O.lib()
+    n = args.cpu_sample_mib * MIB
+    buf = ctypes.create_string_buffer(n)
+    ct = ctypes.create_string_buffer(n)
+    L.oracle_fill_splitmix(buf, 0, n, args.seed)
+    refs = ctypes.create_string_buffer(64 * (n // args.block_size))
+    t = time.perf_counter()
+    L.oracle_post_batch(refs, ct, bytes(32), buf, n, args.block_size, None, 1)
+    dt = time.perf_counter() - t
+    return {"value": round(n / GIB / dt, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{args.cpu_sample_mib} MiB = {n // args.block_size} x "
+                      f"{args.block_size // 1024} KiB blocks, oracle_post_batch, 1 thread, "
+                      f"{dt:.1f} s"}
+
+
+def host_round_trip(N, args, bs):
+    """Host memory -> GPU -> host: glfsx_create over a pageable host buffer with
+    a store sink that receives every ctext + ref on the host (blob.go Writer
+    semantics).  PCIe-inclusive; never the headline value."""
+    import numpy as np
+    n = int(args.host_rt_gib * GIB) // bs * bs
+    if n == 0:
+        return None
+    host = np.empty(n, dtype=np.uint8)
+    from oracle import oracle as O
+    O.lib().oracle_fill_splitmix(host.ctypes.data, 0, min(n, 64 * MIB), args.seed)
+    reps = n // (64 * MIB)
+    for i in range(1, reps):
+        host[i * 64 * MIB:(i + 1) * 64 * MIB] = host[:64 * MIB]
+    seen = [0]
+
+    @N.POST_FN
+    def sink(_ctx, kind, ref, ctext, ln):
+        seen[0] += ln
+        return 0
+
+    root = N.glfsx_root()
+    best = None
+    for _ in range(2):
+        seen[0] = 0
+        t = time.perf_counter()
+        N.check(N.lib.glfsx_create(bs, bs, None, None, host.ctypes.data, n, sink, None,
+                                   ctypes.byref(root)))
+        dt = time.perf_counter() - t
+        best = dt if best is None else min(best, dt)
+    return {"value": round(n / GIB / best, 2), "unit": "GiB/s", "bytes": n,
+            "what": "glfsx_create from pageable host memory, ctext+refs back to host "
+                    "via the store sink (H2D + kernels + D2H)"}
+
+
+if __name__ == "__main__":
+    main()

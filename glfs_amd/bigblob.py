@@ -1,0 +1,262 @@
+"""Python mirror of the reference's bigblob write-path interface.
+
+Reference: bigblob/machine.go, bigblob/blob.go, bigblob/ref.go, bigblob/index.go
+(blobcache/glfs, Go).  Same names (snake_case), same argument meaning, same
+error behaviour (Panic where Go panics, StoreError where Go returns the store
+error).  Everything below is a thin ctypes call into libglfsx.so; the hashing
+and encryption run in the gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import io
+from dataclasses import dataclass
+from typing import BinaryIO, Optional, Protocol, Union
+
+from . import _native as N
+from ._native import Panic, StoreError  # noqa: F401  (re-exported)
+
+DEK_SIZE = 32          # ref.go:16
+CID_SIZE = 32          # blobcache.CIDSize [ext]
+REF_SIZE = CID_SIZE + DEK_SIZE  # ref.go:52
+MAX_REF_SIZE = REF_SIZE         # index.go:6
+KIND_DATA, KIND_INDEX = 0, 1
+
+
+@dataclass(frozen=True)
+class Ref:
+    """ref.go:54-57: Ref{CID, DEK}; binary form CID || DEK (ref.go:77-82)."""
+    cid: bytes
+    dek: bytes
+
+    def marshal_binary(self) -> bytes:
+        return self.cid + self.dek
+
+    @staticmethod
+    def from_bytes(x: bytes) -> "Ref":
+        """ref.go:59-75 RefFromBytes."""
+        if len(x) < REF_SIZE:
+            raise ValueError(f"too small to be ref len={len(x)}")
+        return Ref(bytes(x[:CID_SIZE]), bytes(x[CID_SIZE:REF_SIZE]))
+
+    def to_json(self) -> dict:
+        return {"cid": self.cid.hex(), "dek": self.dek.hex()}
+
+
+@dataclass(frozen=True)
+class Root:
+    """blob.go:17-21 Root{Ref, Size, BlockSize}."""
+    ref: Ref
+    size: int
+    block_size: int
+
+    def equals(self, other: "Root") -> bool:  # blob.go:27-29
+        return (self.size == other.size and self.block_size == other.block_size
+                and self.ref == other.ref)
+
+
+class WO(Protocol):
+    """The write-only store boundary (bcsdk.WO, [ext]): MaxSize + Post.
+    post() receives the ctext and the GPU-computed ref (CID || DEK)."""
+
+    def max_size(self) -> int: ...
+
+    def post(self, ctext: bytes, ref: bytes, kind: int) -> None: ...
+
+
+def _salt_arg(salt: Optional[bytes]) -> Optional[bytes]:
+    if salt is None:
+        return None
+    if len(salt) != 32:
+        raise ValueError("salt must be 32 bytes")
+    return bytes(salt)
+
+
+def derive_key(salt: bytes, data: bytes, out_len: int = 32) -> bytes:
+    """ref.go:152-161 DeriveKey(out, salt, input): BLAKE3 keyed with salt,
+    first out_len XOF bytes (GPU)."""
+    out = ctypes.create_string_buffer(32)
+    data = bytes(data)
+    N.check(N.lib.glfsx_derive_key(out, out_len, _salt_arg(salt), data, len(data)))
+    return out.raw[:out_len]
+
+
+def depth(size: int, block_size: int) -> int:
+    """blob.go:256-264."""
+    return N.lib.glfsx_depth(size, block_size)
+
+
+def branching_factor(block_size: int) -> int:
+    """blob.go:266-268."""
+    return N.lib.glfsx_branching_factor(block_size)
+
+
+def _make_post_cb(store: Optional[WO]):
+    if store is None:
+        return N.POST_FN(0), None
+    errors: list = []
+
+    def cb(_ctx, kind, ref, ctext, n):
+        try:
+            ct = ctypes.string_at(ctext, n) if n else b""
+            store.post(ct, ctypes.string_at(ref, REF_SIZE), kind)
+            return 0
+        except Exception as e:  # surfaced as StoreError
+            errors.append(e)
+            return 1
+
+    return N.POST_FN(cb), errors
+
+
+class Writer:
+    """blob.go:71-83 Writer (NewWriter/Write/Finish)."""
+
+    def __init__(self, machine: "Machine", store: WO, salt: Optional[bytes],
+                 cid_key: Optional[bytes] = None):
+        self._cb, self._errors = _make_post_cb(store)
+        err = ctypes.c_int(0)
+        self._w = N.lib.glfsx_writer_new(machine.block_size, store.max_size(),
+                                         _salt_arg(salt), cid_key, self._cb, None,
+                                         ctypes.byref(err))
+        if not self._w:
+            N.check(err.value)
+
+    def _raise(self, rc: int):
+        if rc == N.GLFSX_E_STORE and self._errors:
+            raise StoreError(rc, repr(self._errors[0])) from self._errors[0]
+        N.check(rc)
+
+    def write(self, data: bytes) -> int:
+        """blob.go:120-133."""
+        data = bytes(data)
+        rc = N.lib.glfsx_writer_write(self._w, data, len(data))
+        if rc:
+            self._raise(rc)
+        return len(data)
+
+    def finish(self) -> Root:
+        """blob.go:135-150."""
+        r = N.glfsx_root()
+        rc = N.lib.glfsx_writer_finish(self._w, ctypes.byref(r))
+        if rc:
+            self._raise(rc)
+        return Root(Ref.from_bytes(bytes(r.ref)), r.size, r.block_size)
+
+    def close(self) -> None:
+        if self._w:
+            N.lib.glfsx_writer_free(self._w)
+            self._w = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _copy(w, r: Union[bytes, bytearray, memoryview, BinaryIO]) -> None:
+    """io.Copy: a bytes-like source is one Write (bytes.Reader is a WriterTo);
+    a stream is copied in 32 KiB pieces."""
+    if isinstance(r, (bytes, bytearray, memoryview)):
+        w.write(r)
+        return
+    while True:
+        piece = r.read(32 * 1024)
+        if not piece:
+            return
+        w.write(piece)
+
+
+class Machine:
+    """bigblob/machine.go:32-55.  block_size 0 = the store's MaxSize."""
+
+    def __init__(self, block_size: int = 0, cache_size: int = 64):
+        if block_size < 0:  # machine.go:24 WithBlockSize panics
+            raise Panic(N.GLFSX_E_ARG, str(block_size))
+        self.block_size = block_size
+        self.cache_size = cache_size
+
+    def new_writer(self, store: WO, salt: Optional[bytes] = None,
+                   cid_key: Optional[bytes] = None) -> Writer:
+        """blob.go:85-114."""
+        return Writer(self, store, salt, cid_key)
+
+    def create(self, store: WO, salt: Optional[bytes], r,
+               cid_key: Optional[bytes] = None) -> Root:
+        """blob.go:209-217."""
+        w = self.new_writer(store, salt, cid_key)
+        try:
+            _copy(w, r)
+            return w.finish()
+        finally:
+            w.close()
+
+
+class MemStore:
+    """In-memory stand-in for blobcache's schema.MemStore [ext].  It keeps
+    (CID -> ctext) as posted by the GPU path (a pre-hashed Post: the CID was
+    computed on the device).  Tests re-verify every CID with the oracle."""
+
+    def __init__(self, max_size: int):
+        self._max = max_size
+        self.blobs: dict[bytes, bytes] = {}
+        self.log: list[tuple[int, bytes, int]] = []  # (kind, ref, len)
+
+    def max_size(self) -> int:
+        return self._max
+
+    def post(self, ctext: bytes, ref: bytes, kind: int = KIND_DATA) -> None:
+        if len(ctext) > self._max:
+            raise ValueError(f"blob too large {len(ctext)} > {self._max}")
+        self.blobs[ref[:CID_SIZE]] = ctext
+        self.log.append((kind, ref, len(ctext)))
+
+    def __len__(self) -> int:
+        return len(self.blobs)
+
+    def exists(self, cid: bytes) -> bool:
+        return cid in self.blobs
+
+    def get(self, cid: bytes) -> bytes:
+        return self.blobs[cid]
+
+
+def crypto_xor(dek: bytes, data: bytes) -> bytes:
+    """ref.go:137-144 cryptoXOR (ChaCha20, zero nonce, counter 0) on the GPU;
+    self-inverse, so it is also getF's decrypt (ref.go:122)."""
+    data = bytes(data)
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    N.check(N.lib.glfsx_chacha20_xor(bytes(dek), data, out, len(data)))
+    return out.raw[:len(data)]
+
+
+def read_all(store: MemStore, root: Root) -> bytes:
+    """Read side (blob.go:31-69 ReadAt/getPiece, ref.go:113-126 getF) for
+    round-trip verification: walk the index tree, decrypt each blob."""
+    bs = root.block_size
+    bf = branching_factor(bs)
+    lvl = depth(root.size, bs)
+
+    def get_f(ref: Ref) -> bytes:
+        return crypto_xor(ref.dek, store.get(ref.cid))
+
+    out = io.BytesIO()
+
+    def walk(ref: Ref, level: int, remaining: int) -> int:
+        data = get_f(ref)
+        if level == 0:
+            out.write(data)
+            return len(data)
+        if len(data) != bf * MAX_REF_SIZE:
+            raise ValueError("data is not correct size for index")
+        got = 0
+        for i in range(bf):
+            if got >= remaining:
+                break
+            child = Ref.from_bytes(data[i * 64:(i + 1) * 64])
+            got += walk(child, level - 1, remaining - got)
+        return got
+
+    if root.size:
+        walk(root.ref, lvl, root.size)
+    return out.getvalue()

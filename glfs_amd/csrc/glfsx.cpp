@@ -1,0 +1,828 @@
+// glfsx.cpp -- host runtime behind include/glfsx.h.
+//
+// C++ mirror of the reference's bigblob write-path interface (the reference is
+// Go; with no Go toolchain in this image the host side above the C-ABI is C++,
+// see DESIGN.md "Boundary").  All hashing/encryption runs in the gfx950
+// kernels of post_kernels.hip; this file only stages bytes, sequences
+// launches and keeps the reference's Writer bookkeeping (blob.go:71-206).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/glfsx.h"
+#include "kernels.h"
+
+using namespace glfsx;
+
+namespace {
+
+thread_local std::string tls_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  tls_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                     \
+  do {                                                                    \
+    hipError_t e_ = (expr);                                               \
+    if (e_ != hipSuccess)                                                 \
+      return fail(GLFSX_E_DEVICE, "%s: %s (%s:%d)", #expr,                \
+                  hipGetErrorString(e_), __FILE__, __LINE__);             \
+  } while (0)
+
+// Grow-only device / pinned-host buffer.
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 4096);
+    HIP_TRY(hipMalloc(&p, want));
+    cap = want;
+    return 0;
+  }
+  uint8_t *u8() const { return static_cast<uint8_t *>(p); }
+};
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 4096);
+    HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+    cap = want;
+    return 0;
+  }
+  uint8_t *u8() const { return static_cast<uint8_t *>(p); }
+};
+
+// Per-thread device context: the library is reentrant because every host
+// thread gets its own stream and staging (bigblob.Writer is single-goroutine,
+// glfs.Machine is used concurrently: SURVEY 8b "Threading").
+struct Ctx {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  DevBuf d_in, d_ct, d_refs, d_lvl_a, d_lvl_b, d_small;
+  PinBuf h_small;
+  ~Ctx() {
+    // Process teardown may already have unloaded the HIP runtime; leak.
+  }
+};
+thread_local Ctx tls_ctx;
+thread_local int tls_dev = 0;
+
+int ctx_get(Ctx **out) {
+  Ctx &c = tls_ctx;
+  if (c.stream == nullptr || c.dev != tls_dev) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+      return fail(GLFSX_E_DEVICE,
+                  "no HIP device available (%s); the glfsx path has no CPU "
+                  "fallback",
+                  e != hipSuccess ? hipGetErrorString(e) : "count = 0");
+    if (tls_dev >= n)
+      return fail(GLFSX_E_DEVICE, "device %d out of range (%d devices)",
+                  tls_dev, n);
+    HIP_TRY(hipSetDevice(tls_dev));
+    if (c.stream && c.dev != tls_dev) c = Ctx();
+    HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    c.dev = tls_dev;
+  } else {
+    HIP_TRY(hipSetDevice(c.dev));
+  }
+  *out = &c;
+  return 0;
+}
+
+hipStream_t pick_stream(Ctx *c, void *stream) {
+  return stream ? static_cast<hipStream_t>(stream) : c->stream;
+}
+
+void salt_words(uint32_t w[8], const uint8_t *salt) {
+  static const uint8_t zero[32] = {0};
+  words_from_key(w, salt ? salt : zero);
+}
+
+void cid_words(PostJob &j, const uint8_t *cid_key) {
+  if (cid_key) {
+    words_from_key(j.cid_key, cid_key);
+    j.cid_keyed = true;
+  } else {
+    blake3_iv_words(j.cid_key);
+    j.cid_keyed = false;
+  }
+}
+
+// DeriveKey on the GPU (ref.go:152-161): keyed BLAKE3 of `in`, 32 bytes.
+int derive_key_dev(Ctx *c, uint8_t out[32], const uint8_t salt[32],
+                   const void *in, size_t n) {
+  if (n > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED, "derive_key input of %zu bytes exceeds %llu",
+                n, (unsigned long long)kMaxMsgLen);
+  if (int e = c->d_small.ensure(64 + n + 64)) return e;
+  if (int e = c->h_small.ensure(64)) return e;
+  uint8_t *d_out = c->d_small.u8();
+  uint8_t *d_in = c->d_small.u8() + 64;
+  if (n) HIP_TRY(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+  PostJob j{};
+  j.src = d_in;
+  j.ctext = nullptr;
+  j.stride = 0;
+  j.msg_len = n;
+  j.last_len = n;
+  j.n = 1;
+  j.out = RefLayout{d_out, ~0ull, 0};
+  salt_words(j.salt, salt);
+  HIP_TRY(launch_keyed_hash(j, 0, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_small.p, d_out, 32, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(out, c->h_small.p, 32);
+  return 0;
+}
+
+int check_block_size(uint64_t bs) {
+  if (bs < GLFSX_MIN_BLOCK_SIZE)
+    return fail(GLFSX_E_BLOCKSIZE_LT_MIN, "blockSize cannot be < %d",
+                GLFSX_MIN_BLOCK_SIZE);
+  if (bs > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED,
+                "block size %llu above the kernels' limit %llu",
+                (unsigned long long)bs, (unsigned long long)kMaxMsgLen);
+  return 0;
+}
+
+struct Salts {
+  uint8_t raw[32], index[32];
+};
+
+// blob.go:99-101
+int derive_salts(Ctx *c, const uint8_t *salt, Salts *s) {
+  static const uint8_t zero[32] = {0};
+  const uint8_t *sl = salt ? salt : zero;
+  if (int e = derive_key_dev(c, s->index, sl, "index", 5)) return e;
+  return derive_key_dev(c, s->raw, sl, "raw", 3);
+}
+
+// Post `nodes` index nodes (each exactly bs bytes) starting at d_nodes;
+// refs go into the next level's node buffer (or dense when out.bf = max).
+int post_level(Ctx *c, hipStream_t s, const uint8_t salt[32],
+               const uint8_t *cid_key, const uint8_t *d_nodes, uint64_t nodes,
+               uint64_t bs, uint8_t *d_ctext, RefLayout out) {
+  PostJob j{};
+  j.src = d_nodes;
+  j.ctext = d_ctext;
+  j.stride = bs;
+  j.msg_len = bs;
+  j.last_len = bs;
+  j.n = nodes;
+  j.out = out;
+  words_from_key(j.salt, salt);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, s));
+  return 0;
+}
+
+// Build the levels above a level whose refs sit in `cur` as `nodes` zero-
+// padded index nodes (closed form of blob.go:165-206).
+int build_up(Ctx *c, hipStream_t s, const Salts &salts, const uint8_t *cid_key,
+             uint64_t bs, uint8_t *cur, uint64_t nodes, DevBuf *spare,
+             uint8_t root_ref[64], uint64_t *posts) {
+  const uint64_t bf = bs / 64;
+  for (;;) {
+    if (int e = c->d_ct.ensure(nodes * bs)) return e;
+    if (nodes == 1) {
+      if (int e = c->d_refs.ensure(64)) return e;
+      if (int e = post_level(c, s, salts.index, cid_key, cur, 1, bs,
+                             c->d_ct.u8(), RefLayout{c->d_refs.u8(), ~0ull, 0}))
+        return e;
+      *posts += 1;
+      HIP_TRY(hipMemcpyAsync(root_ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      return 0;
+    }
+    const uint64_t m = (nodes + bf - 1) / bf;
+    if (int e = spare->ensure(m * bs)) return e;
+    HIP_TRY(hipMemsetAsync(spare->p, 0, m * bs, s));
+    if (int e = post_level(c, s, salts.index, cid_key, cur, nodes, bs,
+                           c->d_ct.u8(), RefLayout{spare->u8(), bf, bs}))
+      return e;
+    *posts += nodes;
+    cur = spare->u8();
+    nodes = m;
+    spare = (spare == &c->d_lvl_a) ? &c->d_lvl_b : &c->d_lvl_a;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ Writer
+// bigblob/blob.go:71-83.  Data blocks are staged in a pinned batch and hashed
+// on the GPU together; Post calls and index bookkeeping then replay the
+// reference's exact order (postBuf -> addRef -> maybe post index node).
+struct glfsx_writer {
+  Ctx *c = nullptr;
+  uint64_t bs = 0, bf = 0;
+  Salts salts{};
+  uint8_t cid_key[32]{};
+  bool has_cid_key = false;
+  glfsx_post_fn post = nullptr;
+  void *post_ctx = nullptr;
+  std::vector<std::vector<uint8_t>> indexes;  // index.go Index per level
+  std::vector<uint64_t> counts;
+  uint64_t size = 0;
+  // batch staging
+  PinBuf h_in, h_ct, h_refs;
+  DevBuf d_in;  // per-writer so concurrent writers on one thread don't clash
+  uint64_t batch_blocks = 1;
+  uint64_t full = 0;     // complete blocks staged
+  uint64_t partial = 0;  // bytes of the block being filled
+  int sticky = 0;        // first error; the writer is dead afterwards
+};
+
+namespace {
+
+const uint8_t *cidk(const glfsx_writer *w) {
+  return w->has_cid_key ? w->cid_key : nullptr;
+}
+
+// Post one message from host memory (ref.go:98 post + sink), synchronously.
+int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
+             const uint8_t *data, uint64_t n, uint8_t ref[64]) {
+  Ctx *c = w->c;
+  if (int e = c->d_in.ensure(n + 64)) return e;
+  if (int e = c->d_ct.ensure(n + 64)) return e;
+  if (int e = c->d_refs.ensure(64)) return e;
+  if (int e = w->h_ct.ensure(std::max<uint64_t>(n, w->batch_blocks * w->bs) + 64))
+    return e;
+  if (n)
+    HIP_TRY(hipMemcpyAsync(c->d_in.p, data, n, hipMemcpyHostToDevice, c->stream));
+  PostJob j{};
+  j.src = c->d_in.u8();
+  j.ctext = c->d_ct.u8();
+  j.stride = 0;
+  j.msg_len = n;
+  j.last_len = n;
+  j.n = 1;
+  j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+  words_from_key(j.salt, salt);
+  cid_words(j, cidk(w));
+  HIP_TRY(launch_post(j, c->stream));
+  if (n)
+    HIP_TRY(hipMemcpyAsync(w->h_ct.p, c->d_ct.p, n, hipMemcpyDeviceToHost,
+                           c->stream));
+  if (int e = c->h_small.ensure(64)) return e;
+  HIP_TRY(hipMemcpyAsync(c->h_small.p, c->d_refs.p, 64, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(ref, c->h_small.p, 64);
+  if (w->post) {
+    int rc = w->post(w->post_ctx, kind, ref, w->h_ct.p, n);
+    if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+  }
+  return 0;
+}
+
+// blob.go:165-182
+int add_ref(glfsx_writer *w, size_t i, const uint8_t ref[64]) {
+  if (w->indexes.size() <= i) {
+    w->indexes.emplace_back(w->bs, 0);
+    w->counts.push_back(0);
+  }
+  memcpy(w->indexes[i].data() + w->counts[i] * 64, ref, 64);
+  w->counts[i]++;
+  if (w->counts[i] < w->bf) return 0;
+  uint8_t r2[64];
+  if (int e = post_one(w, 1, w->salts.index, w->indexes[i].data(), w->bs, r2))
+    return e;
+  w->counts[i] = 0;
+  std::fill(w->indexes[i].begin(), w->indexes[i].end(), 0);
+  return add_ref(w, i + 1, r2);
+}
+
+// Hash the staged complete blocks on the GPU, then replay postBuf for each
+// (blob.go:152-163) in order.
+int flush(glfsx_writer *w) {
+  if (w->full == 0) return 0;
+  Ctx *c = w->c;
+  const uint64_t nbytes = w->full * w->bs;
+  if (int e = w->d_in.ensure(nbytes)) return e;
+  if (int e = c->d_ct.ensure(nbytes)) return e;
+  if (int e = c->d_refs.ensure(w->full * 64)) return e;
+  if (int e = w->h_ct.ensure(nbytes + 64)) return e;
+  if (int e = w->h_refs.ensure(w->full * 64)) return e;
+  HIP_TRY(hipMemcpyAsync(w->d_in.p, w->h_in.p, nbytes, hipMemcpyHostToDevice,
+                         c->stream));
+  PostJob j{};
+  j.src = w->d_in.u8();
+  j.ctext = c->d_ct.u8();
+  j.stride = w->bs;
+  j.msg_len = w->bs;
+  j.last_len = w->bs;
+  j.n = w->full;
+  j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+  words_from_key(j.salt, w->salts.raw);
+  cid_words(j, cidk(w));
+  HIP_TRY(launch_post(j, c->stream));
+  HIP_TRY(hipMemcpyAsync(w->h_refs.p, c->d_refs.p, w->full * 64,
+                         hipMemcpyDeviceToHost, c->stream));
+  if (w->post)
+    HIP_TRY(hipMemcpyAsync(w->h_ct.p, c->d_ct.p, nbytes, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (uint64_t b = 0; b < w->full; ++b) {
+    const uint8_t *ref = w->h_refs.u8() + 64 * b;
+    if (w->post) {
+      int rc = w->post(w->post_ctx, 0, ref, w->h_ct.u8() + b * w->bs, w->bs);
+      if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+    }
+    if (int e = add_ref(w, 0, ref)) return e;
+    w->size += w->bs;
+  }
+  if (w->partial)
+    memmove(w->h_in.u8(), w->h_in.u8() + nbytes, w->partial);
+  w->full = 0;
+  return 0;
+}
+
+// blob.go:184-206
+int finish_indexes(glfsx_writer *w, uint8_t out[64]) {
+  for (size_t i = 0; i < w->indexes.size(); ++i) {
+    if (i + 1 == w->indexes.size()) {
+      if (w->counts[i] == 0)
+        return post_one(w, 1, w->salts.index, nullptr, 0, out);
+      if (w->counts[i] == 1) {
+        memcpy(out, w->indexes[i].data(), 64);
+        return 0;
+      }
+    }
+    if (w->counts[i] > 0) {
+      uint8_t r[64];
+      if (int e = post_one(w, 1, w->salts.index, w->indexes[i].data(), w->bs, r))
+        return e;
+      if (int e = add_ref(w, i + 1, r)) return e;
+    }
+  }
+  return fail(GLFSX_E_ARG, "should not happen");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *glfsx_last_error(void) { return tls_err.c_str(); }
+
+const char *glfsx_version(void) { return "glfsx 0.1 gfx950"; }
+
+int glfsx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int glfsx_set_device(int dev) {
+  if (dev < 0) return fail(GLFSX_E_ARG, "negative device");
+  tls_dev = dev;
+  Ctx *c;
+  return ctx_get(&c);
+}
+
+int glfsx_derive_key(uint8_t *out, size_t out_len, const uint8_t salt[32],
+                     const void *input, size_t n) {
+  if (!out || !salt || (n && !input)) return fail(GLFSX_E_ARG, "null argument");
+  if (out_len > 32)
+    return fail(GLFSX_E_UNSUPPORTED, "derive_key out_len %zu > 32", out_len);
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  uint8_t full[32];
+  if (int e = derive_key_dev(c, full, salt, input, n)) return e;
+  memcpy(out, full, out_len);
+  return 0;
+}
+
+int glfsx_post_batch_device(const uint8_t salt[32], const void *d_ptext,
+                            uint64_t total, uint64_t block_size, void *d_ctext,
+                            void *d_refs, const uint8_t *cid_key,
+                            void *stream) {
+  if (!salt || !d_refs || (total && !d_ptext))
+    return fail(GLFSX_E_ARG, "null argument");
+  if (block_size == 0 || block_size > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED, "block size %llu unsupported",
+                (unsigned long long)block_size);
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  const uint64_t n = (total + block_size - 1) / block_size;
+  if (n == 0) return 0;
+  PostJob j{};
+  j.src = static_cast<const uint8_t *>(d_ptext);
+  j.ctext = static_cast<uint8_t *>(d_ctext);
+  j.stride = block_size;
+  j.msg_len = block_size;
+  j.last_len = total - (n - 1) * block_size;
+  j.n = n;
+  j.out = RefLayout{static_cast<uint8_t *>(d_refs), ~0ull, 0};
+  words_from_key(j.salt, salt);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, pick_stream(c, stream)));
+  return 0;
+}
+
+// Shared setup for the device batch entry points.
+static int batch_job(PostJob *j, const void *d_ptext, uint64_t total,
+                     uint64_t block_size, void *d_ctext, void *d_refs) {
+  if (!d_refs || (total && !d_ptext)) return fail(GLFSX_E_ARG, "null argument");
+  if (block_size == 0 || block_size > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED, "block size %llu unsupported",
+                (unsigned long long)block_size);
+  const uint64_t n = (total + block_size - 1) / block_size;
+  *j = PostJob{};
+  j->src = static_cast<const uint8_t *>(d_ptext);
+  j->ctext = static_cast<uint8_t *>(d_ctext);
+  j->stride = block_size;
+  j->msg_len = block_size;
+  j->last_len = n ? total - (n - 1) * block_size : 0;
+  j->n = n;
+  j->out = RefLayout{static_cast<uint8_t *>(d_refs), ~0ull, 0};
+  return 0;
+}
+
+int glfsx_dek_batch_device(const uint8_t salt[32], const void *d_ptext,
+                           uint64_t total, uint64_t block_size, void *d_refs,
+                           void *stream) {
+  if (!salt) return fail(GLFSX_E_ARG, "null salt");
+  PostJob j;
+  if (int e = batch_job(&j, d_ptext, total, block_size, nullptr, d_refs)) return e;
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  words_from_key(j.salt, salt);
+  HIP_TRY(launch_keyed_hash(j, 32, pick_stream(c, stream)));
+  return 0;
+}
+
+int glfsx_cid_batch_device(const void *d_ptext, uint64_t total,
+                           uint64_t block_size, void *d_ctext, void *d_refs,
+                           const uint8_t *cid_key, void *stream) {
+  PostJob j;
+  if (int e = batch_job(&j, d_ptext, total, block_size, d_ctext, d_refs)) return e;
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  cid_words(j, cid_key);
+  HIP_TRY(launch_cid_pass(j, pick_stream(c, stream)));
+  return 0;
+}
+
+int glfsx_post_batch(const uint8_t salt[32], const void *ptext, uint64_t total,
+                     uint64_t block_size, void *ctext_out, uint8_t *refs_out,
+                     const uint8_t *cid_key) {
+  if (!salt || !refs_out || (total && !ptext))
+    return fail(GLFSX_E_ARG, "null argument");
+  if (block_size == 0 || block_size > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED, "block size %llu unsupported",
+                (unsigned long long)block_size);
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  const uint64_t n = (total + block_size - 1) / block_size;
+  if (n == 0) return 0;
+  // Stage in slabs of whole blocks (<= 256 MiB) to bound device memory.
+  const uint64_t slab_blocks =
+      std::max<uint64_t>(1, (256ull << 20) / block_size);
+  for (uint64_t b0 = 0; b0 < n; b0 += slab_blocks) {
+    const uint64_t nb = std::min(slab_blocks, n - b0);
+    const uint64_t off = b0 * block_size;
+    const uint64_t bytes = std::min<uint64_t>(nb * block_size, total - off);
+    if (int e = c->d_in.ensure(bytes + 64)) return e;
+    if (int e = c->d_ct.ensure(bytes + 64)) return e;
+    if (int e = c->d_refs.ensure(nb * 64)) return e;
+    HIP_TRY(hipMemcpyAsync(c->d_in.p, static_cast<const uint8_t *>(ptext) + off,
+                           bytes, hipMemcpyHostToDevice, c->stream));
+    PostJob j{};
+    j.src = c->d_in.u8();
+    j.ctext = c->d_ct.u8();
+    j.stride = block_size;
+    j.msg_len = block_size;
+    j.last_len = bytes - (nb - 1) * block_size;
+    j.n = nb;
+    j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+    words_from_key(j.salt, salt);
+    cid_words(j, cid_key);
+    HIP_TRY(launch_post(j, c->stream));
+    HIP_TRY(hipMemcpyAsync(refs_out + 64 * b0, c->d_refs.p, nb * 64,
+                           hipMemcpyDeviceToHost, c->stream));
+    if (ctext_out)
+      HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(ctext_out) + off, c->d_ct.p,
+                             bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return 0;
+}
+
+glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
+                               const uint8_t *salt, const uint8_t *cid_key,
+                               glfsx_post_fn post, void *post_ctx, int *err) {
+  int dummy;
+  if (!err) err = &dummy;
+  uint64_t bs = store_max;  // blob.go:86
+  if (block_size > 0) bs = block_size;
+  if (bs > store_max) {  // blob.go:90-92
+    *err = fail(GLFSX_E_BLOCKSIZE_GT_MAX, "blockSize %llu > maxSize %llu",
+                (unsigned long long)bs, (unsigned long long)store_max);
+    return nullptr;
+  }
+  if (int e = check_block_size(bs)) {  // blob.go:93-95
+    *err = e;
+    return nullptr;
+  }
+  Ctx *c;
+  if (int e = ctx_get(&c)) {
+    *err = e;
+    return nullptr;
+  }
+  auto *w = new glfsx_writer();
+  w->c = c;
+  w->bs = bs;
+  w->bf = bs / 64;  // blob.go:107
+  if (int e = derive_salts(c, salt, &w->salts)) {
+    delete w;
+    *err = e;
+    return nullptr;
+  }
+  if (cid_key) {
+    memcpy(w->cid_key, cid_key, 32);
+    w->has_cid_key = true;
+  }
+  w->post = post;
+  w->post_ctx = post_ctx;
+  w->indexes.emplace_back(bs, 0);  // blob.go:111
+  w->counts.push_back(0);
+  w->batch_blocks = std::max<uint64_t>(1, (64ull << 20) / bs);
+  *err = 0;
+  return w;
+}
+
+// blob.go:120-133: a block is complete exactly when buffered + incoming
+// reaches bs; it is staged and hashed with the rest of its batch.
+int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  if (w->sticky) return w->sticky;
+  if (n && !data) return fail(GLFSX_E_ARG, "null data");
+  const uint8_t *p = static_cast<const uint8_t *>(data);
+  if (int e = w->h_in.ensure((w->batch_blocks + 1) * w->bs)) return w->sticky = e;
+  while (n) {
+    const uint64_t room = w->bs - w->partial;
+    const uint64_t take = std::min<uint64_t>(room, n);
+    memcpy(w->h_in.u8() + w->full * w->bs + w->partial, p, take);
+    w->partial += take;
+    p += take;
+    n -= take;
+    if (w->partial == w->bs) {
+      w->full++;
+      w->partial = 0;
+      if (w->full == w->batch_blocks)
+        if (int e = flush(w)) return w->sticky = e;
+    }
+  }
+  return 0;
+}
+
+int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
+  if (!w || !out) return fail(GLFSX_E_ARG, "null argument");
+  if (w->sticky) return w->sticky;
+  if (int e = flush(w)) return w->sticky = e;
+  if (w->partial) {  // blob.go:136-140: the tail block, never padded
+    uint8_t ref[64];
+    if (int e = post_one(w, 0, w->salts.raw, w->h_in.u8(), w->partial, ref))
+      return w->sticky = e;
+    if (int e = add_ref(w, 0, ref)) return w->sticky = e;
+    w->size += w->partial;
+    w->partial = 0;
+  }
+  uint8_t root[64];
+  if (int e = finish_indexes(w, root)) return w->sticky = e;
+  memcpy(out->ref, root, 64);
+  out->size = w->size;
+  out->block_size = w->bs;
+  return 0;
+}
+
+void glfsx_writer_free(glfsx_writer *w) {
+  if (!w) return;
+  if (w->h_in.p) (void)hipHostFree(w->h_in.p);
+  if (w->h_ct.p) (void)hipHostFree(w->h_ct.p);
+  if (w->h_refs.p) (void)hipHostFree(w->h_refs.p);
+  if (w->d_in.p) (void)hipFree(w->d_in.p);
+  delete w;
+}
+
+int glfsx_create(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
+                 const uint8_t *cid_key, const void *data, uint64_t size,
+                 glfsx_post_fn post, void *post_ctx, glfsx_root *out) {
+  int err = 0;
+  glfsx_writer *w =
+      glfsx_writer_new(block_size, store_max, salt, cid_key, post, post_ctx, &err);
+  if (!w) return err;
+  int e = glfsx_writer_write(w, data, size);
+  if (!e) e = glfsx_writer_finish(w, out);
+  glfsx_writer_free(w);
+  return e;
+}
+
+int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
+                        const uint8_t *cid_key, const void *d_data,
+                        uint64_t size, void *d_ctext, glfsx_root *out,
+                        uint64_t *n_posts, void *stream) {
+  if (!out || (size && !d_data)) return fail(GLFSX_E_ARG, "null argument");
+  if (int e = check_block_size(block_size)) return e;
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  hipStream_t s = pick_stream(c, stream);
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  const uint64_t bs = block_size, bf = bs / 64;
+  const uint64_t n0 = (size + bs - 1) / bs;
+  uint64_t posts = 0;
+  if (n0 <= 1) {
+    // n0 == 0: post(indexSalt, nil) (blob.go:187-189); n0 == 1: the only
+    // data block's ref is the root (blob.go:190-193).
+    if (int e = c->d_refs.ensure(64)) return e;
+    if (int e = c->d_small.ensure(64)) return e;
+    PostJob j{};
+    j.src = n0 ? static_cast<const uint8_t *>(d_data) : c->d_small.u8();
+    j.ctext = n0 ? static_cast<uint8_t *>(d_ctext) : nullptr;
+    j.stride = 0;
+    j.msg_len = size;
+    j.last_len = size;
+    j.n = 1;
+    j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+    words_from_key(j.salt, n0 ? salts.raw : salts.index);
+    cid_words(j, cid_key);
+    HIP_TRY(launch_post(j, s));
+    HIP_TRY(hipMemcpyAsync(out->ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    posts = 1;
+  } else {
+    const uint64_t n1 = (n0 + bf - 1) / bf;
+    if (int e = c->d_lvl_a.ensure(n1 * bs)) return e;
+    HIP_TRY(hipMemsetAsync(c->d_lvl_a.p, 0, n1 * bs, s));
+    PostJob j{};
+    j.src = static_cast<const uint8_t *>(d_data);
+    j.ctext = static_cast<uint8_t *>(d_ctext);
+    j.stride = bs;
+    j.msg_len = bs;
+    j.last_len = size - (n0 - 1) * bs;
+    j.n = n0;
+    j.out = RefLayout{c->d_lvl_a.u8(), bf, bs};
+    words_from_key(j.salt, salts.raw);
+    cid_words(j, cid_key);
+    HIP_TRY(launch_post(j, s));
+    posts = n0;
+    if (int e = build_up(c, s, salts, cid_key, bs, c->d_lvl_a.u8(), n1,
+                         &c->d_lvl_b, out->ref, &posts))
+      return e;
+  }
+  out->size = size;
+  out->block_size = bs;
+  if (n_posts) *n_posts = posts;
+  return 0;
+}
+
+int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
+                       const uint8_t *cid_key, const void *d_range,
+                       uint64_t size, uint64_t first_block, uint64_t nb,
+                       void *d_ctext, uint8_t *level1_out, void *stream) {
+  if (!level1_out || (nb && !d_range)) return fail(GLFSX_E_ARG, "null argument");
+  if (int e = check_block_size(block_size)) return e;
+  const uint64_t bs = block_size, bf = bs / 64;
+  const uint64_t n0 = (size + bs - 1) / bs;
+  if (first_block % bf)
+    return fail(GLFSX_E_ARG, "shard start %llu not a multiple of bf=%llu",
+                (unsigned long long)first_block, (unsigned long long)bf);
+  if (nb == 0 || first_block + nb > n0 || n0 < 2)
+    return fail(GLFSX_E_ARG, "bad shard range");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  hipStream_t s = pick_stream(c, stream);
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  const bool has_last = first_block + nb == n0;
+  const uint64_t m = (nb + bf - 1) / bf;
+  if (int e = c->d_lvl_a.ensure(m * bs)) return e;
+  if (int e = c->d_ct.ensure(m * bs)) return e;
+  if (int e = c->d_refs.ensure(m * 64)) return e;
+  HIP_TRY(hipMemsetAsync(c->d_lvl_a.p, 0, m * bs, s));
+  PostJob j{};
+  j.src = static_cast<const uint8_t *>(d_range);
+  j.ctext = static_cast<uint8_t *>(d_ctext);
+  j.stride = bs;
+  j.msg_len = bs;
+  j.last_len = has_last ? size - (n0 - 1) * bs : bs;
+  j.n = nb;
+  j.out = RefLayout{c->d_lvl_a.u8(), bf, bs};
+  words_from_key(j.salt, salts.raw);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, s));
+  if (int e = post_level(c, s, salts.index, cid_key, c->d_lvl_a.u8(), m, bs,
+                         c->d_ct.u8(), RefLayout{c->d_refs.u8(), ~0ull, 0}))
+    return e;
+  HIP_TRY(hipMemcpyAsync(level1_out, c->d_refs.p, m * 64, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
+                           const uint8_t *cid_key, const uint8_t *level1,
+                           uint64_t n1, uint64_t size, glfsx_root *out) {
+  if (!level1 || !out || n1 == 0) return fail(GLFSX_E_ARG, "null argument");
+  if (int e = check_block_size(block_size)) return e;
+  const uint64_t bs = block_size, bf = bs / 64;
+  const uint64_t n0 = (size + bs - 1) / bs;
+  if (n0 < 2 || (n0 + bf - 1) / bf != n1)
+    return fail(GLFSX_E_ARG, "level-1 count %llu does not match size",
+                (unsigned long long)n1);
+  out->size = size;
+  out->block_size = bs;
+  if (n1 == 1) {
+    memcpy(out->ref, level1, 64);
+    return 0;
+  }
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  const uint64_t m = (n1 + bf - 1) / bf;
+  if (int e = c->d_lvl_a.ensure(m * bs)) return e;
+  HIP_TRY(hipMemsetAsync(c->d_lvl_a.p, 0, m * bs, c->stream));
+  // scatter the gathered refs into zero-padded nodes (index.go:33-38)
+  for (uint64_t k = 0; k < m; ++k) {
+    const uint64_t cnt = std::min(bf, n1 - k * bf);
+    HIP_TRY(hipMemcpyAsync(c->d_lvl_a.u8() + k * bs, level1 + k * bf * 64,
+                           cnt * 64, hipMemcpyHostToDevice, c->stream));
+  }
+  uint64_t posts = 0;
+  return build_up(c, c->stream, salts, cid_key, bs, c->d_lvl_a.u8(), m,
+                  &c->d_lvl_b, out->ref, &posts);
+}
+
+int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
+                       uint64_t n) {
+  if (!dek || (n && (!src || !dst))) return fail(GLFSX_E_ARG, "null argument");
+  if (n == 0) return 0;
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  if (int e = c->d_in.ensure(n)) return e;
+  if (int e = c->d_ct.ensure(n)) return e;
+  HIP_TRY(hipMemcpyAsync(c->d_in.p, src, n, hipMemcpyHostToDevice, c->stream));
+  uint32_t k[8];
+  words_from_key(k, dek);
+  HIP_TRY(launch_chacha_xor(k, c->d_in.u8(), c->d_ct.u8(), n, c->stream));
+  HIP_TRY(hipMemcpyAsync(dst, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int glfsx_fill_splitmix_device(void *d_dst, uint64_t offset, uint64_t n,
+                               uint64_t seed, void *stream) {
+  if (n && !d_dst) return fail(GLFSX_E_ARG, "null argument");
+  if (offset & 7) return fail(GLFSX_E_ARG, "offset must be a multiple of 8");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  HIP_TRY(launch_fill(static_cast<uint8_t *>(d_dst), offset, n, seed,
+                      pick_stream(c, stream)));
+  return 0;
+}
+
+// blob.go:219-268 (pure integer shape math, no hashing)
+static uint64_t log2_ceil(uint64_t x) {
+  int l = 64 - __builtin_clzll(x);
+  if (__builtin_popcountll(x) > 1) l++;
+  return uint64_t(l) - 1;
+}
+static uint64_t div_ceil(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+uint64_t glfsx_branching_factor(uint64_t block_size) { return block_size / 64; }
+
+int glfsx_depth(uint64_t size, uint64_t block_size) {
+  if (size == 0) return 0;
+  const uint64_t blocks = div_ceil(size, block_size);
+  const uint64_t bf = glfsx_branching_factor(block_size);
+  return int(div_ceil(log2_ceil(blocks), log2_ceil(bf)));
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// kernels.h -- internal interface between the host runtime (glfsx.cpp) and the
+// gfx950 kernels (post_kernels.hip).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace glfsx {
+
+// Where ref j of a pass lands: refs + (j / ref_bf) * ref_stride + (j % ref_bf) * 64.
+// Dense output: ref_bf = UINT64_MAX, ref_stride = 0.  Index-node output:
+// ref_bf = bf, ref_stride = block_size (bigblob/index.go:33-38: slot i of a
+// node is bytes [64i, 64i+64), the rest of the node stays zero).
+struct RefLayout {
+  uint8_t *refs;
+  uint64_t bf;
+  uint64_t stride;
+};
+
+// One "post" of n equal messages (the last one possibly short) laid out at
+// src + j*stride: DEK pass then ChaCha20+CID pass (bigblob/ref.go:98-161).
+struct PostJob {
+  const uint8_t *src;
+  uint8_t *ctext;       // nullable; may alias src
+  uint64_t stride;      // bytes between message starts
+  uint64_t msg_len;     // length of messages 0..n-2
+  uint64_t last_len;    // length of message n-1
+  uint64_t n;           // number of messages (>= 1)
+  RefLayout out;
+  uint32_t salt[8];     // DEK key words (little-endian words of the salt)
+  uint32_t cid_key[8];  // CID key words (IV when unkeyed)
+  bool cid_keyed;
+};
+
+// Largest message the workgroup-per-message kernels accept (256 lanes x 64
+// BLAKE3 chunks).
+constexpr uint64_t kMaxMsgLen = 256ull * 64 * 1024;
+
+hipError_t launch_post(const PostJob &job, hipStream_t s);
+
+// The second half of launch_post alone: ChaCha20 keyed by the DEK already in
+// bytes [32,64) of each ref slot, ctext store, CID into bytes [0,32).
+hipError_t launch_cid_pass(const PostJob &job, hipStream_t s);
+
+// DEK-only pass (keyed BLAKE3, first 32 XOF bytes) over the same layout,
+// writing 32-byte digests to out (at byte offset `out_off` of each ref slot).
+hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
+                             hipStream_t s);
+
+// ChaCha20 XOR (zero nonce, counter 0) of n bytes with key words k.
+hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
+                             uint8_t *dst, uint64_t n, hipStream_t s);
+
+// Synthetic splitmix64 byte stream (see oracle_fill_splitmix); offset % 8 == 0.
+hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
+                       hipStream_t s);
+
+void words_from_key(uint32_t w[8], const uint8_t key[32]);
+void blake3_iv_words(uint32_t w[8]);
+
+}  // namespace glfsx

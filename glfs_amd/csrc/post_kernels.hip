@@ -1,0 +1,555 @@
+// post_kernels.hip -- gfx950 kernels for the bigblob write path.
+//
+// Per bigblob block ("message"), bigblob/ref.go:98-161 computes
+//   DEK  = BLAKE3-keyed(salt, ptext)[0:32]                 (ref.go:146-161)
+//   ctext = ChaCha20(DEK, nonce 0^12, counter 0) ^ ptext    (ref.go:137-144)
+//   CID  = BLAKE3-256(ctext)   (store.Post, ref.go:103; blobcache [ext])
+// Both hashes are BLAKE3 trees over 1 KiB chunks of 64 B blocks.
+//
+// Mapping (DESIGN.md "Kernels"):
+//   * one 256-lane workgroup per message; lane t owns the G consecutive
+//     BLAKE3 chunks [t*G, t*G+G) (G = power of two, template parameter) and
+//     reduces them in registers to one subtree chaining value;
+//   * the 16-word message schedule is applied at compile time (fully unrolled
+//     rounds, the permutation is register renaming -- no LDS, no shuffles);
+//   * the 256 subtree CVs are merged pairwise through LDS; the pairwise merge
+//     with an odd element passing through is exactly BLAKE3's left-complete
+//     tree, and the final parent gets ROOT;
+//   * the ChaCha20 pass uses the message's DEK as wave-uniform SGPR operands
+//     and fuses keystream XOR, the ctext store and the CID compression, so
+//     ptext is read once per pass and ctext is never re-read.
+// Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
+#include "kernels.h"
+
+namespace glfsx {
+namespace {
+
+constexpr uint32_t kIV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u,
+                             0xA54FF53Au, 0x510E527Fu, 0x9B05688Cu,
+                             0x1F83D9ABu, 0x5BE0CD19u};
+enum : uint32_t {
+  kChunkStart = 1,
+  kChunkEnd = 2,
+  kParent = 4,
+  kRoot = 8,
+  kKeyed = 16,
+};
+
+struct Sched {
+  int s[7][16];
+};
+constexpr Sched make_sched() {
+  constexpr int perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  Sched t{};
+  for (int i = 0; i < 16; ++i) t.s[0][i] = i;
+  for (int r = 1; r < 7; ++r)
+    for (int i = 0; i < 16; ++i) t.s[r][i] = t.s[r - 1][perm[i]];
+  return t;
+}
+constexpr Sched kSched = make_sched();
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+
+#define B3G(a, b, c, d, x, y) \
+  a = a + b + (x);            \
+  d = rotr(d ^ a, 16);        \
+  c = c + d;                  \
+  b = rotr(b ^ c, 12);        \
+  a = a + b + (y);            \
+  d = rotr(d ^ a, 8);         \
+  c = c + d;                  \
+  b = rotr(b ^ c, 7);
+
+template <int R>
+__device__ __forceinline__ void b3_round(uint32_t (&v)[16],
+                                         const uint32_t (&m)[16]) {
+  constexpr const int *s = kSched.s[R];
+  B3G(v[0], v[4], v[8], v[12], m[s[0]], m[s[1]]);
+  B3G(v[1], v[5], v[9], v[13], m[s[2]], m[s[3]]);
+  B3G(v[2], v[6], v[10], v[14], m[s[4]], m[s[5]]);
+  B3G(v[3], v[7], v[11], v[15], m[s[6]], m[s[7]]);
+  B3G(v[0], v[5], v[10], v[15], m[s[8]], m[s[9]]);
+  B3G(v[1], v[6], v[11], v[12], m[s[10]], m[s[11]]);
+  B3G(v[2], v[7], v[8], v[13], m[s[12]], m[s[13]]);
+  B3G(v[3], v[4], v[9], v[14], m[s[14]], m[s[15]]);
+}
+
+// cv <- first 8 words of compress(cv, m, counter, block_len, flags): the
+// chaining value, or for a ROOT compression the first 32 output bytes
+// (XOF block 0), which is all the write path ever reads.
+__device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
+                                            const uint32_t (&m)[16],
+                                            uint32_t ctr_lo, uint32_t ctr_hi,
+                                            uint32_t blen, uint32_t flags) {
+  uint32_t v[16] = {cv[0],  cv[1],  cv[2],  cv[3],  cv[4],  cv[5],
+                    cv[6],  cv[7],  kIV[0], kIV[1], kIV[2], kIV[3],
+                    ctr_lo, ctr_hi, blen,   flags};
+  b3_round<0>(v, m);
+  b3_round<1>(v, m);
+  b3_round<2>(v, m);
+  b3_round<3>(v, m);
+  b3_round<4>(v, m);
+  b3_round<5>(v, m);
+  b3_round<6>(v, m);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
+}
+
+#define CQR(a, b, c, d) \
+  a += b;               \
+  d = rotr(d ^ a, 16);  \
+  c += d;               \
+  b = rotr(b ^ c, 20);  \
+  a += b;               \
+  d = rotr(d ^ a, 24);  \
+  c += d;               \
+  b = rotr(b ^ c, 25);
+
+// RFC 8439 block function, nonce 0^12 (ref.go:138), 32-bit block counter.
+__device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
+                                             const uint32_t (&k)[8],
+                                             uint32_t ctr) {
+  constexpr uint32_t c0 = 0x61707865u, c1 = 0x3320646eu, c2 = 0x79622d32u,
+                     c3 = 0x6b206574u;
+  x[0] = c0;
+  x[1] = c1;
+  x[2] = c2;
+  x[3] = c3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[4 + i] = k[i];
+  x[12] = ctr;
+  x[13] = 0;
+  x[14] = 0;
+  x[15] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    CQR(x[0], x[4], x[8], x[12]);
+    CQR(x[1], x[5], x[9], x[13]);
+    CQR(x[2], x[6], x[10], x[14]);
+    CQR(x[3], x[7], x[11], x[15]);
+    CQR(x[0], x[5], x[10], x[15]);
+    CQR(x[1], x[6], x[11], x[12]);
+    CQR(x[2], x[7], x[8], x[13]);
+    CQR(x[3], x[4], x[9], x[14]);
+  }
+  x[0] += c0;
+  x[1] += c1;
+  x[2] += c2;
+  x[3] += c3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[4 + i] += k[i];
+  x[12] += ctr;
+}
+
+// 64-byte message block at p with `avail` valid bytes (zero padded).
+template <bool ALIGNED>
+__device__ __forceinline__ void load_block(uint32_t (&m)[16], const uint8_t *p,
+                                           uint32_t avail) {
+  if (ALIGNED && avail >= 64) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    m[0] = w0.x; m[1] = w0.y; m[2] = w0.z; m[3] = w0.w;
+    m[4] = w1.x; m[5] = w1.y; m[6] = w1.z; m[7] = w1.w;
+    m[8] = w2.x; m[9] = w2.y; m[10] = w2.z; m[11] = w2.w;
+    m[12] = w3.x; m[13] = w3.y; m[14] = w3.z; m[15] = w3.w;
+  } else {
+    const uint32_t lim = avail < 64 ? avail : 64;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t idx = 4 * i + b;
+        if (idx < lim) w |= uint32_t(p[idx]) << (8 * b);
+      }
+      m[i] = w;
+    }
+  }
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void store_block(uint8_t *p, const uint32_t (&c)[16],
+                                            uint32_t avail) {
+  if (ALIGNED && avail >= 64) {
+    uint4 *q = reinterpret_cast<uint4 *>(p);
+    q[0] = make_uint4(c[0], c[1], c[2], c[3]);
+    q[1] = make_uint4(c[4], c[5], c[6], c[7]);
+    q[2] = make_uint4(c[8], c[9], c[10], c[11]);
+    q[3] = make_uint4(c[12], c[13], c[14], c[15]);
+  } else {
+    const uint32_t lim = avail < 64 ? avail : 64;
+    for (uint32_t idx = 0; idx < lim; ++idx)
+      p[idx] = uint8_t(c[idx >> 2] >> (8 * (idx & 3)));
+  }
+}
+
+// Zero the bytes of m at and beyond `avail` (only called when avail < 64).
+__device__ __forceinline__ void mask_tail(uint32_t (&m)[16], uint32_t avail) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t lo = 4 * i;
+    uint32_t keep;
+    if (lo + 4 <= avail) keep = 0xffffffffu;
+    else if (lo >= avail) keep = 0u;
+    else keep = (1u << (8 * (avail - lo))) - 1u;
+    m[i] &= keep;
+  }
+}
+
+constexpr int ilog2(int g) { return g <= 1 ? 0 : 1 + ilog2(g / 2); }
+
+struct KArgs {
+  const uint8_t *src;
+  uint8_t *ctext;
+  uint64_t stride, msg_len, last_len, n;
+  uint8_t *refs;
+  uint64_t ref_bf, ref_stride;
+  uint32_t key[8];
+  uint32_t base;     // kKeyed or 0
+  uint32_t out_off;  // byte offset of the 32-byte result inside the ref slot
+};
+
+// Lane-local subtree over chunks [first, first+n_my) of one message: returns
+// its chaining value in cv (or the root output when `whole`: this lane holds
+// the entire message).  Eager merges after chunk jj = ctz(jj+1), final merges
+// right to left: the same tree as BLAKE3's incremental hasher.
+template <int G, bool CHACHA, bool ALIGNED>
+__device__ __forceinline__ void lane_subtree(
+    uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint64_t len,
+    uint32_t first, uint32_t n_my, bool whole, const uint32_t (&key)[8],
+    uint32_t base, const uint32_t (&dek)[8]) {
+  constexpr int D = ilog2(G);
+  uint32_t stk[D > 0 ? D : 1][8];
+  uint32_t depth = 0;
+  for (uint32_t jj = 0; jj < n_my; ++jj) {
+    const uint32_t chunk = first + jj;
+    const uint64_t coff = uint64_t(chunk) << 10;
+    const uint64_t rem = len - coff;
+    const uint32_t clen = rem < 1024 ? uint32_t(rem) : 1024u;
+    const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
+    const bool last = jj + 1 == n_my;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = key[i];
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t boff = b << 6;
+      const uint32_t avail = clen - boff;
+      uint32_t m[16];
+      load_block<ALIGNED>(m, msg + coff + boff, avail);
+      if constexpr (CHACHA) {
+        uint32_t x[16];
+        chacha_block(x, dek, (chunk << 4) + b);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+        if (avail < 64) mask_tail(m, avail);
+        if (cmsg) store_block<ALIGNED>(cmsg + coff + boff, m, avail);
+      }
+      uint32_t fl = base;
+      if (b == 0) fl |= kChunkStart;
+      if (b + 1 == nb) {
+        fl |= kChunkEnd;
+        if (whole && n_my == 1) fl |= kRoot;
+      }
+      b3_compress(cv, m, chunk, 0u, avail < 64 ? avail : 64u, fl);
+    }
+    if constexpr (D > 0) {
+      const uint32_t merges = last ? depth : uint32_t(__builtin_ctz(jj + 1));
+      for (uint32_t i = 0; i < merges; ++i) {
+        uint32_t m[16];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          m[w] = stk[0][w];
+          m[8 + w] = cv[w];
+          cv[w] = key[w];
+        }
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d)
+#pragma unroll
+          for (int w = 0; w < 8; ++w) stk[d][w] = stk[d + 1][w];
+        --depth;
+        const uint32_t fl =
+            base | kParent | ((whole && last && depth == 0) ? kRoot : 0u);
+        b3_compress(cv, m, 0u, 0u, 64u, fl);
+      }
+      if (!last) {
+#pragma unroll
+        for (int d = D - 1; d > 0; --d)
+#pragma unroll
+          for (int w = 0; w < 8; ++w) stk[d][w] = stk[d - 1][w];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) stk[0][w] = cv[w];
+        ++depth;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t *w,
+                                             uint32_t lane) {
+  // lanes 0..7 write one word each
+  if (lane < 8) {
+    const uint32_t v = w[lane];
+    uint8_t *p = dst + 4 * lane;
+    if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+      *reinterpret_cast<uint32_t *>(p) = v;
+    } else {
+      p[0] = uint8_t(v);
+      p[1] = uint8_t(v >> 8);
+      p[2] = uint8_t(v >> 16);
+      p[3] = uint8_t(v >> 24);
+    }
+  }
+}
+
+template <int G, bool CHACHA, bool ALIGNED>
+__global__ __launch_bounds__(256) void k_pass(KArgs a) {
+  __shared__ uint32_t lds[256 * 8];
+  const uint64_t j = blockIdx.x;
+  const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
+  const uint8_t *msg = a.src + j * a.stride;
+  uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + j * a.stride : nullptr;
+  uint8_t *ref = a.refs + (j / a.ref_bf) * a.ref_stride + (j % a.ref_bf) * 64;
+  const uint32_t t = threadIdx.x;
+
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = a.key[i];
+  uint32_t dek[8];
+  if constexpr (CHACHA) {
+    // DEK written by the preceding pass into bytes [32,64) of this ref slot.
+    const uint8_t *dp = ref + 32;
+    if ((reinterpret_cast<uintptr_t>(dp) & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        dek[i] = __builtin_amdgcn_readfirstlane(
+            reinterpret_cast<const uint32_t *>(dp)[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        dek[i] = __builtin_amdgcn_readfirstlane(
+            uint32_t(dp[4 * i]) | (uint32_t(dp[4 * i + 1]) << 8) |
+            (uint32_t(dp[4 * i + 2]) << 16) | (uint32_t(dp[4 * i + 3]) << 24));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dek[i] = 0;
+  }
+
+  const uint32_t C = len ? uint32_t((len + 1023) >> 10) : 1u;
+  const bool whole = C <= uint32_t(G);
+  const uint32_t first = t * G;
+  const uint32_t n_my = first < C ? min(uint32_t(G), C - first) : 0u;
+  uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (n_my)
+    lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
+                                     key, a.base, dek);
+  if (whole) {  // uniform: depends on len only
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[i] = cv[i];
+    }
+    __syncthreads();
+    store_digest(ref + a.out_off, lds, t);
+    return;
+  }
+  const uint32_t active = (C + G - 1) / G;
+  if (t < active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
+  }
+  __syncthreads();
+  uint32_t k = active;
+  while (k > 1) {
+    const uint32_t half = k >> 1, odd = k & 1u;
+    uint32_t p[8];
+    if (t < half) {
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        m[i] = lds[(2 * t) * 8 + i];
+        m[8 + i] = lds[(2 * t + 1) * 8 + i];
+        p[i] = key[i];
+      }
+      b3_compress(p, m, 0u, 0u, 64u, a.base | kParent | (k == 2 ? kRoot : 0u));
+    } else if (odd && t == half) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p[i] = lds[(k - 1) * 8 + i];
+    }
+    __syncthreads();
+    if (t < half + odd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[t * 8 + i] = p[i];
+    }
+    __syncthreads();
+    k = half + odd;
+  }
+  store_digest(ref + a.out_off, lds, t);
+}
+
+__global__ __launch_bounds__(256) void k_chacha_xor(KArgs a) {
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k[i] = a.key[i];
+  const uint64_t nblk = (a.msg_len + 63) >> 6;
+  for (uint64_t b = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; b < nblk;
+       b += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t off = b << 6;
+    const uint64_t rem = a.msg_len - off;
+    const uint32_t avail = rem < 64 ? uint32_t(rem) : 64u;
+    uint32_t m[16], x[16];
+    const bool al = ((reinterpret_cast<uintptr_t>(a.src + off) |
+                      reinterpret_cast<uintptr_t>(a.ctext + off)) & 15) == 0;
+    if (al) load_block<true>(m, a.src + off, avail);
+    else load_block<false>(m, a.src + off, avail);
+    chacha_block(x, k, uint32_t(b));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+    if (al) store_block<true>(a.ctext + off, m, avail);
+    else store_block<false>(a.ctext + off, m, avail);
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Synthetic data (bench/test inputs): byte o = byte (o & 7) of
+// splitmix64(seed ^ (o >> 3)); same generator as oracle_fill_splitmix.
+__global__ __launch_bounds__(256) void k_fill(uint8_t *dst, uint64_t offset,
+                                              uint64_t n, uint64_t seed) {
+  const uint64_t words = (n + 7) >> 3;
+  for (uint64_t w = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; w < words;
+       w += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t v = splitmix64(seed ^ ((offset >> 3) + w));
+    if ((w + 1) * 8 <= n && ((reinterpret_cast<uintptr_t>(dst) & 7) == 0)) {
+      reinterpret_cast<uint64_t *>(dst)[w] = v;
+    } else {
+      for (uint64_t i = w * 8; i < n && i < w * 8 + 8; ++i)
+        dst[i] = uint8_t(v >> (8 * (i & 7)));
+    }
+  }
+}
+
+template <int G, bool CHACHA>
+hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
+  const dim3 grid(uint32_t(a.n)), block(256);
+  if (aligned)
+    hipLaunchKernelGGL((k_pass<G, CHACHA, true>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_pass<G, CHACHA, false>), grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+template <bool CHACHA>
+hipError_t launch_pass(const KArgs &a, uint64_t maxlen, bool aligned,
+                       hipStream_t s) {
+  const uint64_t C = maxlen ? (maxlen + 1023) >> 10 : 1;
+  int g = 1;
+  while (256ull * g < C) g *= 2;
+  switch (g) {
+    case 1: return launch_g<1, CHACHA>(a, aligned, s);
+    case 2: return launch_g<2, CHACHA>(a, aligned, s);
+    case 4: return launch_g<4, CHACHA>(a, aligned, s);
+    case 8: return launch_g<8, CHACHA>(a, aligned, s);
+    case 16: return launch_g<16, CHACHA>(a, aligned, s);
+    case 32: return launch_g<32, CHACHA>(a, aligned, s);
+    case 64: return launch_g<64, CHACHA>(a, aligned, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+KArgs make_args(const PostJob &job) {
+  KArgs a{};
+  a.src = job.src;
+  a.ctext = job.ctext;
+  a.stride = job.stride;
+  a.msg_len = job.msg_len;
+  a.last_len = job.last_len;
+  a.n = job.n;
+  a.refs = job.out.refs;
+  a.ref_bf = job.out.bf;
+  a.ref_stride = job.out.stride;
+  return a;
+}
+
+bool is_aligned(const PostJob &job) {
+  const uintptr_t x = reinterpret_cast<uintptr_t>(job.src) |
+                      reinterpret_cast<uintptr_t>(job.ctext) |
+                      uintptr_t(job.stride);
+  return (x & 15) == 0;
+}
+
+}  // namespace
+
+void words_from_key(uint32_t w[8], const uint8_t key[32]) {
+  for (int i = 0; i < 8; ++i)
+    w[i] = uint32_t(key[4 * i]) | (uint32_t(key[4 * i + 1]) << 8) |
+           (uint32_t(key[4 * i + 2]) << 16) | (uint32_t(key[4 * i + 3]) << 24);
+}
+
+void blake3_iv_words(uint32_t w[8]) {
+  for (int i = 0; i < 8; ++i) w[i] = kIV[i];
+}
+
+hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
+                             hipStream_t s) {
+  if (job.n == 0) return hipSuccess;
+  KArgs a = make_args(job);
+  for (int i = 0; i < 8; ++i) a.key[i] = job.salt[i];
+  a.base = kKeyed;
+  a.out_off = out_off;
+  const uint64_t maxlen = job.n > 1 ? std::max(job.msg_len, job.last_len)
+                                    : job.last_len;
+  return launch_pass<false>(a, maxlen, is_aligned(job), s);
+}
+
+hipError_t launch_post(const PostJob &job, hipStream_t s) {
+  if (job.n == 0) return hipSuccess;
+  hipError_t e = launch_keyed_hash(job, 32, s);
+  if (e != hipSuccess) return e;
+  return launch_cid_pass(job, s);
+}
+
+hipError_t launch_cid_pass(const PostJob &job, hipStream_t s) {
+  if (job.n == 0) return hipSuccess;
+  KArgs a = make_args(job);
+  for (int i = 0; i < 8; ++i) a.key[i] = job.cid_key[i];
+  a.base = job.cid_keyed ? kKeyed : 0u;
+  a.out_off = 0;
+  const uint64_t maxlen = job.n > 1 ? std::max(job.msg_len, job.last_len)
+                                    : job.last_len;
+  return launch_pass<true>(a, maxlen, is_aligned(job), s);
+}
+
+hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
+                       hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (offset & 7) return hipErrorInvalidValue;
+  const uint64_t words = (n + 7) >> 3;
+  uint64_t grid = (words + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(k_fill, dim3(uint32_t(grid)), dim3(256), 0, s, dst, offset,
+                     n, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
+                             uint8_t *dst, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  KArgs a{};
+  a.src = src;
+  a.ctext = dst;
+  a.msg_len = n;
+  for (int i = 0; i < 8; ++i) a.key[i] = k[i];
+  const uint64_t nblk = (n + 63) >> 6;
+  uint64_t grid = (nblk + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(k_chacha_xor, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace glfsx

@@ -1,0 +1,111 @@
+"""Python mirror of the reference's glfs typed-object write API.
+
+Reference: glfs.go:12-97, machine.go:12-66, blob.go:15-39 (blobcache/glfs).
+Quirk kept for parity: NewMachine ignores its options, so the machine salt is
+always 0^32 (machine.go:41-48) and WithSalt has no effect.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+from . import bigblob
+from .bigblob import Root
+
+DEFAULT_BLOCK_SIZE = 1 << 21  # glfs.go:12
+TYPE_BLOB = "blob"            # glfs.go:18
+TYPE_TREE = "tree"            # glfs.go:19
+
+
+@dataclass(frozen=True)
+class Ref:
+    """glfs.go:35-38 Ref{Type, bigblob.Root} (Root embedded/flattened)."""
+    type: str
+    root: Root
+
+    def equals(self, other: "Ref") -> bool:
+        return self.type == other.type and self.root.equals(other.root)
+
+    def to_json(self) -> dict:
+        d = {"type": self.type}
+        d.update(self.root.ref.to_json())
+        d["size"] = self.root.size
+        d["blockSize"] = self.root.block_size
+        return d
+
+
+def with_salt(salt: bytes):
+    """machine.go:15-19 WithSalt -- dead: NewMachine never applies options."""
+    def opt(m: "Machine") -> None:
+        m.salt = salt
+    return opt
+
+
+class TypedWriter:
+    """glfs.go:68-92."""
+
+    def __init__(self, ty: str, bw: bigblob.Writer):
+        self.ty = ty
+        self.bw = bw
+
+    def write(self, data: bytes) -> int:
+        return self.bw.write(data)
+
+    def finish(self) -> Ref:
+        root = self.bw.finish()
+        self.bw.close()
+        return Ref(self.ty, root)
+
+
+class Machine:
+    """machine.go:27-48."""
+
+    def __init__(self, *opts):
+        self.salt = bytes(32)  # opts are ignored (machine.go:41-48)
+        self.block_size = DEFAULT_BLOCK_SIZE
+        self.bbag = bigblob.Machine(block_size=self.block_size)
+
+    def make_salt(self, ty: str) -> bytes:
+        """machine.go:50-54."""
+        return bigblob.derive_key(self.salt, ty.encode())
+
+    def new_typed_writer(self, store, ty: str) -> TypedWriter:
+        """glfs.go:74-76."""
+        return TypedWriter(ty, self.bbag.new_writer(store, self.make_salt(ty)))
+
+    def post_typed(self, store, ty: str, r) -> Ref:
+        """glfs.go:50-57."""
+        tw = self.new_typed_writer(store, ty)
+        try:
+            bigblob._copy(tw, r)
+            return tw.finish()
+        finally:
+            tw.bw.close()
+
+    def post_blob(self, store, r) -> Ref:
+        """blob.go:15-17."""
+        return self.post_typed(store, TYPE_BLOB, r)
+
+    def new_blob_writer(self, store) -> TypedWriter:
+        """blob.go:37-39."""
+        return self.new_typed_writer(store, TYPE_BLOB)
+
+
+_default: Optional[Machine] = None
+
+
+def _default_machine() -> Machine:
+    global _default
+    if _default is None:
+        _default = Machine()
+    return _default
+
+
+def post_typed(store, ty: str, r) -> Ref:
+    """machine.go:59-61."""
+    return _default_machine().post_typed(store, ty, r)
+
+
+def post_blob(store, r) -> Ref:
+    """machine.go:64-66."""
+    return _default_machine().post_blob(store, r)

@@ -1,0 +1,181 @@
+/*
+ * glfsx.h -- C-ABI of the MI355X-native GLFS bigblob write path.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no torch or HIP types
+ * in the signatures (device pointers and streams travel as void*).  A Go
+ * maintainer binds it with cgo; the Python mirror in
+ * glfs_amd/ binds it with ctypes.  Every compute entry point runs on the GPU
+ * (hand-written gfx950 HIP kernels); there is no CPU fallback -- without a
+ * usable HIP device every call fails with GLFSX_E_DEVICE.
+ *
+ * Reference interfaces replaced (reference = blobcache/glfs, Go):
+ *   glfsx_derive_key       bigblob/ref.go:152-161  DeriveKey(out, salt, input)
+ *   glfsx_post_batch*,     bigblob/ref.go:98-111   (*Machine).post, batched over
+ *   glfsx_dek/cid_batch_device
+ *                          equal-size blocks, minus the store.Post call
+ *                          (ref.go:103), which stays with the caller
+ *   glfsx_writer_*         bigblob/blob.go:71-206  Writer: NewWriter/Write/
+ *                          Finish (postBuf/addRef/finishIndexes inside)
+ *   glfsx_create           bigblob/blob.go:209-217 (*Machine).Create
+ *   glfsx_create_device    Create over a device-resident blob (no host copies)
+ *   glfsx_shard_device /   the same, split by disjoint block ranges across
+ *   glfsx_root_from_level1 GPUs; the caller gathers the level-1 refs
+ *   glfsx_depth            bigblob/blob.go:256-264 depth()
+ *   glfsx_chacha20_xor*    bigblob/ref.go:137-144  cryptoXOR (read side decrypt)
+ *
+ * Conventions:
+ *   - 0 = ok, negative = status; glfsx_last_error() gives a thread-local text.
+ *   - Where the reference panics (blob.go:91,94; ref.go:130) the C side returns
+ *     GLFSX_E_BLOCKSIZE_GT_MAX / GLFSX_E_BLOCKSIZE_LT_MIN / GLFSX_E_ARG and the
+ *     binding re-panics; store failures come back as GLFSX_E_STORE with the
+ *     sink's code in glfsx_last_error().
+ *   - The caller owns every buffer; nothing is retained after return (cgo rule).
+ *   - Reentrant: each host thread gets its own HIP stream and staging buffers;
+ *     glfsx_set_device() selects the GPU for the calling thread.
+ *   - Ref layout (ref.go:77-82): 64 bytes = CID[32] || DEK[32].
+ */
+#ifndef GLFSX_H
+#define GLFSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GLFSX_REF_SIZE 64   /* ref.go:52 RefSize = CIDSize + DEKSize */
+#define GLFSX_CID_SIZE 32
+#define GLFSX_DEK_SIZE 32   /* ref.go:16 */
+#define GLFSX_MIN_BLOCK_SIZE 128 /* blob.go:93: 2*maxRefSize */
+
+enum {
+  GLFSX_OK = 0,
+  GLFSX_E_BLOCKSIZE_GT_MAX = -1, /* blob.go:90-92 panic */
+  GLFSX_E_BLOCKSIZE_LT_MIN = -2, /* blob.go:93-95 panic */
+  GLFSX_E_STORE = -3,            /* store.Post returned an error */
+  GLFSX_E_DEVICE = -4,           /* no HIP device / HIP runtime error */
+  GLFSX_E_ARG = -5,              /* invalid argument */
+  GLFSX_E_UNSUPPORTED = -6,      /* e.g. block size above the kernels' limit */
+  GLFSX_E_NOMEM = -7
+};
+
+/* bigblob/blob.go:17-21 Root{Ref, Size, BlockSize} */
+typedef struct glfsx_root {
+  uint8_t ref[GLFSX_REF_SIZE];
+  uint64_t size;
+  uint64_t block_size;
+} glfsx_root;
+
+/* store.Post(ctx, ctext) (ref.go:103).  Called once per posted blob in the
+ * reference's Post order (data blocks and index nodes interleaved exactly as
+ * blob.go:152-206 does).  `ref` is the GPU-computed CID||DEK; a parity-mode
+ * binding compares the store's returned CID with ref[0:32].  kind: 0 = data
+ * block, 1 = index node.  Return 0, or nonzero to abort the write with
+ * GLFSX_E_STORE. */
+typedef int (*glfsx_post_fn)(void *ctx, int kind, const uint8_t *ref,
+                             const void *ctext, uint64_t len);
+
+/* --- runtime ----------------------------------------------------------- */
+const char *glfsx_last_error(void);
+int glfsx_device_count(void);
+int glfsx_set_device(int dev);      /* for the calling thread */
+const char *glfsx_version(void);
+
+/* --- primitives -------------------------------------------------------- */
+/* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input, first out_len
+ * (<= 32) bytes of the XOF. */
+int glfsx_derive_key(uint8_t *out, size_t out_len, const uint8_t salt[32],
+                     const void *input, size_t n);
+
+/* ref.go:98 post() for ceil(total/block_size) blocks of `ptext` (the last one
+ * short), host buffers.  refs_out: 64 bytes per block.  ctext_out nullable.
+ * cid_key: NULL = CID is unkeyed BLAKE3-256(ctext) (blobcache MemStore with
+ * a nil salt); non-NULL = keyed with cid_key. */
+int glfsx_post_batch(const uint8_t salt[32], const void *ptext, uint64_t total,
+                     uint64_t block_size, void *ctext_out, uint8_t *refs_out,
+                     const uint8_t *cid_key);
+
+/* Same, device-resident: d_* are device pointers on the current device;
+ * enqueued on `stream` (hipStream_t, NULL = the thread's stream); returns
+ * without synchronising.  d_ctext nullable; may equal d_ptext (in place). */
+int glfsx_post_batch_device(const uint8_t salt[32], const void *d_ptext,
+                            uint64_t total, uint64_t block_size, void *d_ctext,
+                            void *d_refs, const uint8_t *cid_key, void *stream);
+
+/* The two kernels of glfsx_post_batch_device, separately (profiling and
+ * pipelining): the DEK pass writes DEKs to bytes [32,64) of each ref slot;
+ * the ChaCha20 + CID pass reads them, writes ctext (nullable) and the CIDs to
+ * bytes [0,32).  Same stream semantics as glfsx_post_batch_device. */
+int glfsx_dek_batch_device(const uint8_t salt[32], const void *d_ptext,
+                           uint64_t total, uint64_t block_size, void *d_refs,
+                           void *stream);
+int glfsx_cid_batch_device(const void *d_ptext, uint64_t total,
+                           uint64_t block_size, void *d_ctext, void *d_refs,
+                           const uint8_t *cid_key, void *stream);
+
+/* --- bigblob Writer (blob.go:71-206) ------------------------------------ */
+typedef struct glfsx_writer glfsx_writer;
+
+/* blob.go:85-114.  block_size 0 = store_max (bigblob machine.go:22-30);
+ * salt NULL = 0^32 (blob.go:96-98).  On error returns NULL, *err set. */
+glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
+                               const uint8_t *salt, const uint8_t *cid_key,
+                               glfsx_post_fn post, void *post_ctx, int *err);
+/* blob.go:120-133.  Data blocks are hashed in batches: a store error is
+ * returned by the Write or Finish call whose batch contained the failure. */
+int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n);
+/* blob.go:135-150 */
+int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out);
+void glfsx_writer_free(glfsx_writer *w);
+
+/* blob.go:209-217 Create over an in-memory (host) blob. */
+int glfsx_create(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
+                 const uint8_t *cid_key, const void *data, uint64_t size,
+                 glfsx_post_fn post, void *post_ctx, glfsx_root *out);
+
+/* Create over a device-resident blob: every data block and index node is
+ * posted on the GPU; ctext of the data blocks goes to d_ctext (nullable,
+ * same layout as d_data).  No store callbacks; returns the root.  Writes the
+ * number of posted blobs into *n_posts (nullable). Synchronises `stream`. */
+int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
+                        const uint8_t *cid_key, const void *d_data,
+                        uint64_t size, void *d_ctext, glfsx_root *out,
+                        uint64_t *n_posts, void *stream);
+
+/* Multi-GPU shard: posts blocks [first_block, first_block + nb)
+ * of a blob of `size` bytes whose bytes for that range are at d_range, plus
+ * the level-1 index nodes covering them.  first_block must be a multiple of
+ * bf = block_size/64.  Writes ceil(nb/bf) level-1 refs (64 B each) to
+ * level1_out (host).  Enqueued on stream and synchronised. */
+int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
+                       const uint8_t *cid_key, const void *d_range,
+                       uint64_t size, uint64_t first_block, uint64_t nb,
+                       void *d_ctext, uint8_t *level1_out, void *stream);
+/* Combine the gathered level-1 refs of a blob with n0 > bf data blocks into
+ * its root (levels >= 2 posted on the GPU). */
+int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
+                           const uint8_t *cid_key, const uint8_t *level1,
+                           uint64_t n1, uint64_t size, glfsx_root *out);
+
+/* --- read side (ref.go:113-126 getF decrypt) ---------- */
+/* ChaCha20, zero nonce, counter 0, key = dek (ref.go:137-144). */
+int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
+                       uint64_t n);
+
+/* --- synthetic inputs (bench / tests; not a reference interface) -------- */
+/* Device fill: byte o = byte (o & 7) of splitmix64(seed ^ (o >> 3)) where
+ * splitmix64(x) is the SplitMix64 output function applied to x + golden
+ * gamma; offset must be a multiple of 8.  Same stream as
+ * oracle_fill_splitmix.  Enqueued on stream (NULL = the thread's stream). */
+int glfsx_fill_splitmix_device(void *d_dst, uint64_t offset, uint64_t n,
+                               uint64_t seed, void *stream);
+
+/* --- tree shape (blob.go:219-268) -------------------------------------- */
+int glfsx_depth(uint64_t size, uint64_t block_size);
+uint64_t glfsx_branching_factor(uint64_t block_size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GLFSX_H */

@@ -1,0 +1,366 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle.
+
+Bit-exact on every byte: refs (CID || DEK), ctext, Post order, roots.
+Sizes where the oracle finishes in seconds are compared directly; the 1 GiB
+config-2 blob is compared block by block with the threaded oracle; larger
+device-resident blobs are checked through size-independent properties
+(determinism, in-place == out-of-place, shard/gather == whole, sampled blocks
+against the oracle, decrypt round trip).
+"""
+import ctypes
+import json
+import os
+import random
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KIB, MIB, GIB = 1 << 10, 1 << 20, 1 << 30
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def dev_bytes(torch, n, seed=None, data=None):
+    t = torch.empty(max(n, 1) + 64, dtype=torch.uint8, device="cuda")
+    if data is not None:
+        t[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else t[:0])
+    elif seed is not None:
+        from glfs_amd import _native as N
+        N.check(N.lib.glfsx_fill_splitmix_device(t.data_ptr(), 0, n, seed, None))
+    # torch works on its own stream, glfsx on a per-thread stream: order them
+    torch.cuda.synchronize()
+    return t
+
+
+def zeros(torch, n):
+    t = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    return t
+
+
+def host(t, n):
+    return bytes(t[:n].cpu().numpy().tobytes())
+
+
+# ---------------------------------------------------------------- primitives
+def test_fill_matches_oracle(gpu, O):
+    torch = _torch()
+    for n, seed in [(1, 1), (7, 2), (8, 3), (1000, 4), (1 << 20, 5)]:
+        t = dev_bytes(torch, n, seed=seed)
+        torch.cuda.synchronize()
+        assert host(t, n) == O.fill_splitmix(n, seed)
+
+
+def test_derive_key(gpu, O):
+    from glfs_amd import bigblob
+    rng = random.Random(1)
+    salts = [bytes(32), bytes(range(32)), bytes(rng.randrange(256) for _ in range(32))]
+    sizes = [0, 1, 3, 5, 63, 64, 65, 1023, 1024, 1025, 2048, 3000, 4096, 5000,
+             65536, 262144 + 1, 1 << 20, (2 << 20) + 7]
+    for salt in salts:
+        for n in sizes:
+            data = O.fill_splitmix(n, n + 1)
+            assert bigblob.derive_key(salt, data) == O.derive_key(salt, data), n
+    assert bigblob.derive_key(bytes(32), b"raw", 16) == O.derive_key(bytes(32), b"raw")[:16]
+
+
+def test_crypto_xor(gpu, O):
+    from glfs_amd import bigblob
+    for n in [0, 1, 63, 64, 65, 1000, 4096, 1 << 20]:
+        key = O.fill_splitmix(32, n)
+        data = O.fill_splitmix(n, n + 9)
+        assert bigblob.crypto_xor(key, data) == O.chacha20_xor(data, key)
+
+
+def _post_batch_host(salt, data, bs, cid_key=None):
+    from glfs_amd import _native as N
+    n = (len(data) + bs - 1) // bs
+    refs = ctypes.create_string_buffer(max(64 * n, 1))
+    ct = ctypes.create_string_buffer(max(len(data), 1))
+    N.check(N.lib.glfsx_post_batch(salt, data, len(data), bs, ct, refs, cid_key))
+    return refs.raw[:64 * n], ct.raw[:len(data)]
+
+
+@pytest.mark.parametrize("bs", [128, 1000, 1024, 4096, 65536, 300_000, 1 << 20,
+                                2 << 20, 5 << 20])
+def test_post_batch_vs_oracle(gpu, O, bs):
+    rng = random.Random(bs)
+    salt = bytes(rng.randrange(256) for _ in range(32))
+    for total in sorted({1, bs - 1, bs, bs + 1, 3 * bs + rng.randrange(1, bs),
+                         min(8 * bs, 12 << 20)}):
+        data = O.fill_splitmix(total, total)
+        refs, ct = _post_batch_host(salt, data, bs)
+        for j in range(0, (total + bs - 1) // bs):
+            blk = data[j * bs:(j + 1) * bs]
+            r, c = O.post(salt, blk)
+            assert refs[64 * j:64 * j + 64] == r, (bs, total, j)
+            assert ct[j * bs:j * bs + len(blk)] == c, (bs, total, j)
+
+
+def test_post_batch_keyed_cid(gpu, O):
+    key = bytes(range(100, 132))
+    data = O.fill_splitmix(5 * 4096 + 17, 11)
+    refs, ct = _post_batch_host(bytes(32), data, 4096, cid_key=key)
+    for j in range(6):
+        r, c = O.post(bytes(32), data[j * 4096:(j + 1) * 4096], cid_key=key)
+        assert refs[64 * j:64 * j + 64] == r
+
+
+def test_unaligned_device_pointers(gpu, O):
+    """The byte-load kernel variant (src/ctext not 16-B aligned)."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    bs, total = 4096, 3 * 4096 + 100
+    data = O.fill_splitmix(total, 21)
+    for off in (1, 2, 3, 4, 8):
+        buf = dev_bytes(torch, total + off, data=bytes(off) + data)
+        ctb = zeros(torch, total + 64)
+        refs = zeros(torch, 64 * 4)
+        N.check(N.lib.glfsx_post_batch_device(bytes(32), buf.data_ptr() + off, total, bs,
+                                              ctb.data_ptr() + 3, refs.data_ptr(), None,
+                                              None))
+        torch.cuda.synchronize()
+        rh, ch = host(refs, 256), host(ctb, total + 3)[3:]
+        for j in range(4):
+            r, c = O.post(bytes(32), data[j * bs:(j + 1) * bs])
+            assert rh[64 * j:64 * j + 64] == r, (off, j)
+            assert ch[j * bs:j * bs + len(c)] == c
+
+
+# ------------------------------------------------------------ bigblob writer
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "bigblob.json")))
+
+
+def _data(O, gen, n):
+    if gen == "mod251":
+        return O.mod251(n)
+    if gen.startswith("splitmix:"):
+        return O.fill_splitmix(n, int(gen.split(":")[1]))
+    return gen.split(":", 1)[1].encode()
+
+
+@pytest.mark.parametrize("c", GOLDEN["cases"], ids=lambda c: c["name"])
+def test_golden_vectors(gpu, O, c):
+    from glfs_amd import bigblob
+    data = _data(O, c["gen"], c["size"])
+    salt = bytes.fromhex(c["salt"]) if c["salt"] else None
+    store = bigblob.MemStore(c["block_size"])
+    root = bigblob.Machine(c["block_size"]).create(store, salt, data)
+    assert root.ref.cid.hex() == c["root"]["cid"]
+    assert root.ref.dek.hex() == c["root"]["dek"]
+    assert (root.size, root.block_size) == (c["root"]["size"], c["root"]["blockSize"])
+    assert len(store.log) == c["n_posts"]
+    if "posts" in c:
+        got = [[k, n, r[:32].hex(), r[32:].hex()] for k, r, n in store.log]
+        assert got == c["posts"]
+    # every stored ctext hashes to its CID (the store's own check, ref.go:103)
+    for cid, ct in list(store.blobs.items())[:64]:
+        assert O.blake3(ct) == cid
+    # read side round trip (blob.go:31-69, ref.go:113-126)
+    if c["block_size"] % 64 == 0 and c["size"] <= (4 << 20) + 1:
+        assert bigblob.read_all(store, root) == data
+
+
+def test_glfs_config1(gpu):
+    """examples/write-read-blob: glfs.PostBlob("test data").  With the 1 MiB
+    store of the example the reference panics at HEAD (blob.go:90-92); with a
+    2 MiB store the ref is SURVEY's anchor."""
+    from glfs_amd import _native as N, bigblob, glfs
+    with pytest.raises(N.Panic, match="2097152 > maxSize 1048576"):
+        glfs.post_blob(bigblob.MemStore(1 << 20), b"test data")
+    s = bigblob.MemStore(2 << 20)
+    ref = glfs.post_blob(s, b"test data")
+    assert ref.type == "blob"
+    assert ref.root.ref.cid.hex() == \
+        "c46ac4e44a328b9c07cba45eddb89b635fa44746823f4f5d3f01e39f52a6c851"
+    assert ref.root.ref.dek.hex() == \
+        "d0d02185d4646a367978c907c9b04fd4b7c536467d9c1882a67b2079b8c9841d"
+    assert (ref.root.size, ref.root.block_size) == (9, 2 << 20)
+    assert bigblob.read_all(s, ref.root) == b"test data"
+
+
+def test_writer_streaming_vs_oracle(gpu, O):
+    """Random write granularity; the full Post sequence (kind, ref, ctext) must
+    equal the reference writer's (blob.go:120-206)."""
+    from glfs_amd import bigblob
+    rng = random.Random(3)
+    for bs, size in [(1024, 70_000), (4096, 4096 * 64 * 2 + 5), (128, 20_000),
+                     (1 << 20, 5 * (1 << 20) + 3)]:
+        data = O.fill_splitmix(size, bs)
+        pieces, left = [], size
+        while left:
+            k = min(left, rng.choice([1, 13, bs - 1, bs, bs + 1, 5 * bs + 7, 100_000]))
+            pieces.append(k)
+            left -= k
+        want_root, _, _, want_posts = O.create(data, bs, salt=None, chunks=pieces)
+        store = bigblob.MemStore(bs)
+        w = bigblob.Machine(bs).new_writer(store)
+        off = 0
+        for k in pieces:
+            w.write(data[off:off + k])
+            off += k
+        root = w.finish()
+        w.close()
+        assert root.ref.marshal_binary() == want_root
+        assert [(k, r) for k, r, _ in store.log] == [(k, r) for k, r, _, _ in want_posts]
+        for k, r, _, ct in want_posts:
+            assert store.blobs[r[:32]] == ct
+
+
+def test_store_error_surfaces(gpu, O):
+    from glfs_amd import _native as N, bigblob
+
+    class Flaky(bigblob.MemStore):
+        def post(self, ctext, ref, kind=0):
+            if len(self.log) == 2:
+                raise IOError("disk full")
+            super().post(ctext, ref, kind)
+
+    with pytest.raises(N.StoreError):
+        bigblob.Machine(1024).create(Flaky(1024), None, O.fill_splitmix(10_000, 1))
+
+
+def test_concurrent_writers(gpu, O):
+    """glfs.Machine is used concurrently (machine.go:25): per-thread streams."""
+    from glfs_amd import bigblob
+    results = {}
+
+    def work(i):
+        data = O.fill_splitmix(50_000 + 997 * i, 100 + i)
+        root = bigblob.Machine(4096).create(bigblob.MemStore(4096), None, data)
+        results[i] = (root.ref.marshal_binary(), data)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(6)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for i, (got, data) in results.items():
+        assert got == O.create(data, 4096, salt=None)[0]
+
+
+# ------------------------------------------------------ device-resident path
+def _create_device(torch, bs, t, size, ctext=None, salt=None):
+    from glfs_amd import _native as N
+    r = N.glfsx_root()
+    posts = ctypes.c_uint64()
+    N.check(N.lib.glfsx_create_device(bs, salt, None, t.data_ptr(), size,
+                                      ctext.data_ptr() if ctext is not None else None,
+                                      ctypes.byref(r), ctypes.byref(posts), None))
+    return bytes(r.ref), posts.value
+
+
+@pytest.mark.parametrize("bs,size", [(1 << 20, 0), (1 << 20, 1), (1 << 20, 1 << 20),
+                                     (1 << 20, (17 << 20) + 5), (2 << 20, 64 << 20),
+                                     (1024, 16 * 1024 * 16 + 1), (4096, 3 << 20)])
+def test_create_device_vs_oracle(gpu, O, bs, size):
+    torch = _torch()
+    seed = size + bs
+    t = dev_bytes(torch, size, seed=seed)
+    ct = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    root, posts = _create_device(torch, bs, t, size, ct)
+    data = O.fill_splitmix(size, seed)
+    want, _, _, want_posts = O.create(data, bs, salt=None, closed_form=True)
+    assert root == want
+    assert posts == len(want_posts)
+    got_ct = host(ct, size)
+    for j in range((size + bs - 1) // bs):
+        blk = data[j * bs:(j + 1) * bs]
+        _, c = O.post(O.derive_key(bytes(32), b"raw"), blk)
+        assert got_ct[j * bs:j * bs + len(blk)] == c, j
+
+
+def test_shard_gather_equals_whole(gpu, O):
+    """disjoint block ranges aligned to bf, level-1 refs gathered,
+    root built from them == root of the whole blob == oracle."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    bs = 4096
+    bf = bs // 64
+    size = bs * (bf * 5 + 3) + 777
+    n0 = (size + bs - 1) // bs
+    t = dev_bytes(torch, size, seed=77)
+    whole, _ = _create_device(torch, bs, t, size)
+    want = O.create(O.fill_splitmix(size, 77), bs, salt=None, closed_form=True)[0]
+    assert whole == want
+    for shards in (2, 3, 6):
+        per = -(-n0 // shards)
+        per = -(-per // bf) * bf
+        level1 = b""
+        for b0 in range(0, n0, per):
+            nb = min(per, n0 - b0)
+            out = ctypes.create_string_buffer(64 * (-(-nb // bf)))
+            N.check(N.lib.glfsx_shard_device(bs, None, None, t.data_ptr() + b0 * bs, size,
+                                             b0, nb, None, out, None))
+            level1 += out.raw
+        r = N.glfsx_root()
+        N.check(N.lib.glfsx_root_from_level1(bs, None, None, level1, len(level1) // 64,
+                                             size, ctypes.byref(r)))
+        assert bytes(r.ref) == whole, shards
+
+
+def test_config2_1gib_2mib(gpu, O):
+    """BASELINE config 2: 1 GiB at the glfs default 2 MiB block size
+    (splitmix seed 1): every one of the 512 data refs and the root, bit-exact."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    size, bs = GIB, 2 << 20
+    n0 = size // bs
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    raw = O.derive_key(blob_salt, b"raw")
+    idx = O.derive_key(blob_salt, b"index")
+    t = dev_bytes(torch, size, seed=1)
+    refs = zeros(torch, 64 * n0)
+    N.check(N.lib.glfsx_post_batch_device(raw, t.data_ptr(), size, bs, None,
+                                          refs.data_ptr(), None, None))
+    root, posts = _create_device(torch, bs, t, size, salt=blob_salt)
+    torch.cuda.synchronize()
+    got = host(refs, 64 * n0)
+    L = O.lib()
+    data = ctypes.create_string_buffer(size)
+    L.oracle_fill_splitmix(data, 0, size, 1)
+    want = ctypes.create_string_buffer(64 * n0)
+    L.oracle_post_batch(want, None, raw, data, size, bs, None, 16)
+    assert got == want.raw
+    node = want.raw + bytes(bs - 64 * n0)
+    r_root, _ = O.post(idx, node)
+    assert root == r_root
+    assert posts == n0 + 1
+
+
+def test_large_blob_properties(gpu, O):
+    """4 GiB at 1 MiB, device-resident: determinism, in-place == out-of-place,
+    sampled blocks vs oracle, decrypt of sampled ctext blocks."""
+    torch = _torch()
+    from glfs_amd import _native as N, bigblob
+    size, bs = 4 * GIB, MIB
+    n0 = size // bs
+    raw = O.derive_key(bytes(32), b"raw")
+    t = dev_bytes(torch, size, seed=123)
+    ct = torch.empty(size, dtype=torch.uint8, device="cuda")
+    r1, p1 = _create_device(torch, bs, t, size, ct)
+    r2, p2 = _create_device(torch, bs, t, size)
+    assert r1 == r2 and p1 == p2 == n0 + 1  # n0 < bf: one index node
+    refs = zeros(torch, 64 * n0)
+    N.check(N.lib.glfsx_post_batch_device(raw, t.data_ptr(), size, bs, None,
+                                          refs.data_ptr(), None, None))
+    torch.cuda.synchronize()
+    rh = host(refs, 64 * n0)
+    rng = random.Random(9)
+    for j in [0, 1, n0 - 1] + rng.sample(range(n0), 6):
+        blk = host(t[j * bs:], bs)
+        r, c = O.post(raw, blk)
+        assert rh[64 * j:64 * j + 64] == r, j
+        cth = host(ct[j * bs:], bs)
+        assert cth == c
+        assert bigblob.crypto_xor(r[32:], cth) == blk
+    # in place: ctext over ptext gives the same refs
+    N.check(N.lib.glfsx_post_batch_device(raw, t.data_ptr(), size, bs, t.data_ptr(),
+                                          refs.data_ptr(), None, None))
+    torch.cuda.synchronize()
+    assert host(refs, 64 * n0) == rh
