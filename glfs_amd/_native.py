@@ -90,6 +90,16 @@ if not os.path.exists(LIB_PATH):
         "`python -c 'import __graft_entry__ as g; g.build()'` -- there is no "
         "CPU fallback for the glfsx path")
 
+# PyTorch-ROCm bundles its own libamdhip64.so.7 / libhsa-runtime64.so.  If
+# libglfsx.so were loaded first, /opt/rocm's runtime would be mapped and torch
+# would then bring up a second HIP runtime that sees no GPU.  Importing torch
+# first makes the dynamic linker satisfy our NEEDED libamdhip64.so.7 with the
+# already-loaded runtime, so torch tensors and glfsx share one HIP runtime.
+try:
+    import torch  # noqa: F401
+except ImportError:  # a plain C consumer (e.g. a cgo binding) needs no torch
+    pass
+
 lib = ctypes.CDLL(LIB_PATH)
 for _name, (_res, _args) in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -251,6 +251,8 @@ struct glfsx_writer {
   uint64_t size = 0;
   // batch staging
   PinBuf h_in, h_ct, h_refs;
+  PinBuf h_one;  // ctext of single posts (index nodes, the tail block): must
+                 // not alias h_ct, which flush() is still handing to the sink
   DevBuf d_in;  // per-writer so concurrent writers on one thread don't clash
   uint64_t batch_blocks = 1;
   uint64_t full = 0;     // complete blocks staged
@@ -271,8 +273,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
   if (int e = c->d_in.ensure(n + 64)) return e;
   if (int e = c->d_ct.ensure(n + 64)) return e;
   if (int e = c->d_refs.ensure(64)) return e;
-  if (int e = w->h_ct.ensure(std::max<uint64_t>(n, w->batch_blocks * w->bs) + 64))
-    return e;
+  if (int e = w->h_one.ensure(n + 64)) return e;
   if (n)
     HIP_TRY(hipMemcpyAsync(c->d_in.p, data, n, hipMemcpyHostToDevice, c->stream));
   PostJob j{};
@@ -287,7 +288,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
   cid_words(j, cidk(w));
   HIP_TRY(launch_post(j, c->stream));
   if (n)
-    HIP_TRY(hipMemcpyAsync(w->h_ct.p, c->d_ct.p, n, hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(w->h_one.p, c->d_ct.p, n, hipMemcpyDeviceToHost,
                            c->stream));
   if (int e = c->h_small.ensure(64)) return e;
   HIP_TRY(hipMemcpyAsync(c->h_small.p, c->d_refs.p, 64, hipMemcpyDeviceToHost,
@@ -295,7 +296,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
   HIP_TRY(hipStreamSynchronize(c->stream));
   memcpy(ref, c->h_small.p, 64);
   if (w->post) {
-    int rc = w->post(w->post_ctx, kind, ref, w->h_ct.p, n);
+    int rc = w->post(w->post_ctx, kind, ref, w->h_one.p, n);
     if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
   }
   return 0;
@@ -627,6 +628,7 @@ void glfsx_writer_free(glfsx_writer *w) {
   if (w->h_in.p) (void)hipHostFree(w->h_in.p);
   if (w->h_ct.p) (void)hipHostFree(w->h_ct.p);
   if (w->h_refs.p) (void)hipHostFree(w->h_refs.p);
+  if (w->h_one.p) (void)hipHostFree(w->h_one.p);
   if (w->d_in.p) (void)hipFree(w->d_in.p);
   delete w;
 }

@@ -285,20 +285,21 @@ __device__ __forceinline__ void lane_subtree(
   }
 }
 
-__device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t *w,
-                                             uint32_t lane) {
-  // lanes 0..7 write one word each
-  if (lane < 8) {
-    const uint32_t v = w[lane];
-    uint8_t *p = dst + 4 * lane;
-    if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
-      *reinterpret_cast<uint32_t *>(p) = v;
-    } else {
-      p[0] = uint8_t(v);
-      p[1] = uint8_t(v >> 8);
-      p[2] = uint8_t(v >> 16);
-      p[3] = uint8_t(v >> 24);
-    }
+// One lane writes the 32-byte result (CID or DEK) into its ref slot.  The
+// slot is 16-B aligned for dense refs; index-node slots (node*bs + 64*i) may
+// not be when bs % 16 != 0.
+__device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t (&w)[8]) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
+  if ((a & 15) == 0) {
+    uint4 *q = reinterpret_cast<uint4 *>(dst);
+    q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else if ((a & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t *>(dst)[i] = w[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) dst[i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
   }
 }
 
@@ -344,13 +345,8 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   if (n_my)
     lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
                                      key, a.base, dek);
-  if (whole) {  // uniform: depends on len only
-    if (t == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) lds[i] = cv[i];
-    }
-    __syncthreads();
-    store_digest(ref + a.out_off, lds, t);
+  if (whole) {  // uniform: depends on len only; lane 0 holds the root output
+    if (t == 0) store_digest(ref + a.out_off, cv);
     return;
   }
   const uint32_t active = (C + G - 1) / G;
@@ -383,8 +379,9 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
     }
     __syncthreads();
     k = half + odd;
+    // the last level (k == 2 -> 1) is computed by lane 0: the ROOT output
+    if (k == 1 && t == 0) store_digest(ref + a.out_off, p);
   }
-  store_digest(ref + a.out_off, lds, t);
 }
 
 __global__ __launch_bounds__(256) void k_chacha_xor(KArgs a) {
