@@ -29,10 +29,14 @@ sys.path.insert(0, ROOT)
 
 GIB, MIB = 1 << 30, 1 << 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz
-# int-VALU ops per plaintext byte (DESIGN.md "Rooflines"): BLAKE3 compression
-# ~700 ops / 64 B (x 1.06 for parents), ChaCha20 block ~1010 ops / 64 B.
-OPS_PER_BYTE = {"dek": 700 * 1.06 / 64, "cid": (1010 + 700 * 1.06) / 64}
+# int-VALU roofline (DESIGN.md "Rooflines"): gfx950 issues the 3-input integer
+# ops this path lives on (v_add3_u32, v_alignbit_b32) at 16 lanes/clk/SIMD and
+# mixed ARX streams at ~4 cycles per wave64 instruction (tools/opbench.hip,
+# tools/gmix2.hip): 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
+VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+# VALU lane-instructions per plaintext byte, measured with rocprofv3
+# SQ_INSTS_VALU x 64 / bytes (profiles/r1/summary.json).
+INSTR_PER_BYTE = {"dek": 12.11, "cid": 27.12}
 
 
 def parse():
@@ -61,21 +65,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev = local % max(1, ndev)   # >1 rank per GPU only when rehearsing on 1 GPU
+    torch.cuda.set_device(dev)
+    N.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    N.set_device(local if world > 1 else 0)
+        # gloo carries only the 256-B level-1 gather, the barriers and the
+        # max-over-ranks time: no collective on the data path.
+        dist.init_process_group(os.environ.get("GLFS_DIST_BACKEND", "gloo"))
 
+    from glfs_amd import shard
     bs = args.block_size
     bf = bs // 64
-    per = int(args.size_gib * GIB) // bs * bs      # bytes per rank, whole blocks
-    nb = per // bs
-    assert nb % bf == 0 or world == 1, "per-rank range must be bf-aligned"
-    total = per * world
+    per_req = int(args.size_gib * GIB) // bs * bs   # bytes per rank, whole blocks
+    if world > 1:
+        per_req = max(bf, per_req // bs // bf * bf) * bs   # bf-aligned shards
+    total = per_req * world
     n0 = total // bs
-    first = rank * nb
+    first, nb = shard.plan(total, bs, world)[rank]
+    per = nb * bs
 
     stream = torch.cuda.Stream()
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -89,24 +97,28 @@ def main():
 
     root = N.glfsx_root()
     n_posts = ctypes.c_uint64()
-    lvl1 = ctypes.create_string_buffer(64 * max(1, -(-nb // bf)))
+    root_ref = [b""]
 
     def step():
         if world == 1:
             N.check(N.lib.glfsx_create_device(bs, None, None, data.data_ptr(), per, ct_ptr,
                                               ctypes.byref(root), ctypes.byref(n_posts), sp))
+            root_ref[0] = bytes(root.ref)
             return
-        N.check(N.lib.glfsx_shard_device(bs, None, None, data.data_ptr(), total, first, nb,
-                                         ct_ptr, lvl1, sp))
-        m = -(-nb // bf)
-        mine = torch.frombuffer(bytearray(lvl1.raw[:64 * m]), dtype=torch.uint8).cuda()
-        gathered = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(gathered, mine)  # 256 B per rank: the only exchange
+        lvl1 = shard.shard_device(N, bs, None, None, data.data_ptr(), total, first, nb,
+                                  ct_ptr, sp)
+        mine = torch.frombuffer(bytearray(lvl1), dtype=torch.uint8)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64))
+        cap = int(max(t.item() for t in sizes))
+        padded = torch.zeros(cap, dtype=torch.uint8)
+        padded[:mine.numel()] = mine
+        gathered = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(gathered, padded)   # the only exchange: 64 B per bf blocks
         if rank == 0:
-            allrefs = b"".join(bytes(g.cpu().numpy().tobytes()) for g in gathered)
-            N.check(N.lib.glfsx_root_from_level1(bs, None, None, allrefs,
-                                                 len(allrefs) // 64, total,
-                                                 ctypes.byref(root)))
+            allrefs = b"".join(bytes(g[:int(n.item())].numpy().tobytes())
+                               for g, n in zip(gathered, sizes))
+            root_ref[0] = shard.root_from_level1(N, bs, None, None, allrefs, total)
 
     def barrier():
         if world > 1:
@@ -123,7 +135,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3
@@ -142,12 +154,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (splitmix64 byte stream, generated in HBM)",
-        "config": {"workload": f"bigblob write {args.size_gib:g} GiB/GPU @ {bs // 1024} KiB "
+        "config": {"workload": f"bigblob write {per / GIB:g} GiB/GPU @ {bs // 1024} KiB "
                                f"blocks, device-resident, ctext {'off' if ctext is None else 'to HBM'}",
                    "blob_bytes": total, "block_size": bs, "blocks": n0,
                    "posts_per_step": n_posts.value if world == 1 else None,
                    "parallelism": f"disjoint block ranges x{world}"},
-        "root_cid": bytes(root.ref[:32]).hex() if rank == 0 else None,
+        "root_cid": root_ref[0][:32].hex() if rank == 0 else None,
     }
 
     if rank == 0 and not args.no_extras:
@@ -201,9 +213,9 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             "algorithmic_bytes_per_launch": alg[dom],
             "avg_ms": {k: round(v, 4) for k, v in avg.items()},
             "hashed_GBps": {k: round(per / (v * 1e-3) / 1e9, 1) for k, v in avg.items()}}
-    ops = {k: OPS_PER_BYTE[k] * per for k in avg}
-    valu = {"bound": "valu", "unit": "Tops/s", "peak": round(VALU_PEAK_TOPS, 2),
-            "ops_per_byte": {k: round(v, 2) for k, v in OPS_PER_BYTE.items()},
+    ops = {k: INSTR_PER_BYTE[k] * per for k in avg}
+    valu = {"bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_PEAK_TOPS, 2),
+            "instr_per_byte": INSTR_PER_BYTE,
             "achieved": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12, 2) for k in avg},
             "frac": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 3)
                      for k in avg}}

@@ -211,6 +211,102 @@ struct KArgs {
   uint32_t out_off;  // byte offset of the 32-byte result inside the ref slot
 };
 
+// Merge step after the last block of local chunk jj: pop/parent/push on the
+// lane's CV stack (eager merges = ctz(jj+1); final merges empty the stack).
+template <int D>
+__device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
+                                           uint32_t (&stk)[D > 0 ? D : 1][8],
+                                           uint32_t &depth, uint32_t jj,
+                                           bool last, bool whole,
+                                           const uint32_t (&key)[8],
+                                           uint32_t base) {
+  if constexpr (D > 0) {
+    const uint32_t merges = last ? depth : uint32_t(__builtin_ctz(jj + 1));
+    for (uint32_t i = 0; i < merges; ++i) {
+      uint32_t m[16];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        m[w] = stk[0][w];
+        m[8 + w] = cv[w];
+        cv[w] = key[w];
+      }
+#pragma unroll
+      for (int d = 0; d + 1 < D; ++d)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) stk[d][w] = stk[d + 1][w];
+      --depth;
+      const uint32_t fl =
+          base | kParent | ((whole && last && depth == 0) ? kRoot : 0u);
+      b3_compress(cv, m, 0u, 0u, 64u, fl);
+    }
+    if (!last) {
+#pragma unroll
+      for (int d = D - 1; d > 0; --d)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) stk[d][w] = stk[d - 1][w];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) stk[0][w] = cv[w];
+      ++depth;
+    }
+  }
+}
+
+// Fast path: the lane's G chunks are all full (16*G consecutive 64-B blocks,
+// 16-B aligned).  One loop over the blocks with the next block's four 16-B
+// loads issued before the current compression, so the wave does not stall
+// on HBM latency between blocks.
+template <int G, bool CHACHA>
+__device__ __forceinline__ void lane_subtree_full(
+    uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
+    bool whole, const uint32_t (&key)[8], uint32_t base,
+    const uint32_t (&dek)[8]) {
+  constexpr int D = ilog2(G);
+  uint32_t stk[D > 0 ? D : 1][8];
+  uint32_t depth = 0;
+  const uint4 *q = reinterpret_cast<const uint4 *>(msg + (uint64_t(first) << 10));
+  uint4 *cq = cmsg ? reinterpret_cast<uint4 *>(cmsg + (uint64_t(first) << 10))
+                   : nullptr;
+  uint4 n0 = q[0], n1 = q[1], n2 = q[2], n3 = q[3];
+  for (uint32_t blk = 0; blk < 16u * G; ++blk) {
+    uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w,
+                      n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+    if (blk + 1 < 16u * G) {
+      const uint4 *nq = q + 4 * (blk + 1);
+      n0 = nq[0];
+      n1 = nq[1];
+      n2 = nq[2];
+      n3 = nq[3];
+    }
+    const uint32_t b = blk & 15u, jj = blk >> 4;
+    const uint32_t chunk = first + jj;
+    if (b == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cv[i] = key[i];
+    }
+    if constexpr (CHACHA) {
+      uint32_t x[16];
+      chacha_block(x, dek, (chunk << 4) + b);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+      if (cq) {
+        uint4 *o = cq + 4 * blk;
+        o[0] = make_uint4(m[0], m[1], m[2], m[3]);
+        o[1] = make_uint4(m[4], m[5], m[6], m[7]);
+        o[2] = make_uint4(m[8], m[9], m[10], m[11]);
+        o[3] = make_uint4(m[12], m[13], m[14], m[15]);
+      }
+    }
+    uint32_t fl = base;
+    if (b == 0) fl |= kChunkStart;
+    if (b == 15) {
+      fl |= kChunkEnd;
+      if (whole && G == 1) fl |= kRoot;
+    }
+    b3_compress(cv, m, chunk, 0u, 64u, fl);
+    if (b == 15) lane_merge<D>(cv, stk, depth, jj, jj + 1 == G, whole, key, base);
+  }
+}
+
 // Lane-local subtree over chunks [first, first+n_my) of one message: returns
 // its chaining value in cv (or the root output when `whole`: this lane holds
 // the entire message).  Eager merges after chunk jj = ctz(jj+1), final merges
@@ -253,35 +349,7 @@ __device__ __forceinline__ void lane_subtree(
       }
       b3_compress(cv, m, chunk, 0u, avail < 64 ? avail : 64u, fl);
     }
-    if constexpr (D > 0) {
-      const uint32_t merges = last ? depth : uint32_t(__builtin_ctz(jj + 1));
-      for (uint32_t i = 0; i < merges; ++i) {
-        uint32_t m[16];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-          m[w] = stk[0][w];
-          m[8 + w] = cv[w];
-          cv[w] = key[w];
-        }
-#pragma unroll
-        for (int d = 0; d + 1 < D; ++d)
-#pragma unroll
-          for (int w = 0; w < 8; ++w) stk[d][w] = stk[d + 1][w];
-        --depth;
-        const uint32_t fl =
-            base | kParent | ((whole && last && depth == 0) ? kRoot : 0u);
-        b3_compress(cv, m, 0u, 0u, 64u, fl);
-      }
-      if (!last) {
-#pragma unroll
-        for (int d = D - 1; d > 0; --d)
-#pragma unroll
-          for (int w = 0; w < 8; ++w) stk[d][w] = stk[d - 1][w];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) stk[0][w] = cv[w];
-        ++depth;
-      }
-    }
+    lane_merge<D>(cv, stk, depth, jj, last, whole, key, base);
   }
 }
 
@@ -342,9 +410,13 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   const uint32_t first = t * G;
   const uint32_t n_my = first < C ? min(uint32_t(G), C - first) : 0u;
   uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (n_my)
+  if (ALIGNED && n_my == uint32_t(G) &&
+      len >= (uint64_t(first) + G) << 10) {
+    lane_subtree_full<G, CHACHA>(cv, msg, cmsg, first, whole, key, a.base, dek);
+  } else if (n_my) {
     lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
                                      key, a.base, dek);
+  }
   if (whole) {  // uniform: depends on len only; lane 0 holds the root output
     if (t == 0) store_digest(ref + a.out_off, cv);
     return;

@@ -1,0 +1,49 @@
+"""Multi-GPU sharding of one bigblob write.
+
+Each rank owns a contiguous range of data blocks that starts on a multiple
+of bf = block_size/64, so the level-1 index nodes over its range are entirely
+its own (bigblob/index.go:33-38, blob.go:165-182).  A rank posts its blocks
+and its level-1 nodes on its GPU (glfsx_shard_device); the only exchange is
+a gather of the level-1 refs (64 B per bf blocks: 256 B for a 64 GiB shard at
+1 MiB blocks) after which one rank builds levels >= 2 and the root
+(glfsx_root_from_level1).  No collective touches the data path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Tuple
+
+
+def plan(size: int, block_size: int, world: int) -> List[Tuple[int, int]]:
+    """Block ranges (first_block, n_blocks) per rank, bf-aligned starts, as
+    even as the alignment allows.  Ranks past the end get (n0, 0)."""
+    bf = block_size // 64
+    n0 = -(-size // block_size)
+    groups = -(-n0 // bf)                     # level-1 nodes
+    out = []
+    for r in range(world):
+        g0 = groups * r // world
+        g1 = groups * (r + 1) // world
+        b0 = min(n0, g0 * bf)
+        b1 = min(n0, g1 * bf)
+        out.append((b0, b1 - b0))
+    return out
+
+
+def shard_device(N, block_size: int, salt, cid_key, d_range: int, size: int,
+                 first_block: int, nb: int, d_ctext, stream) -> bytes:
+    """Post blocks [first_block, first_block+nb) (bytes at device pointer
+    d_range) and their level-1 nodes; returns the level-1 refs."""
+    bf = block_size // 64
+    m = -(-nb // bf)
+    out = ctypes.create_string_buffer(64 * max(m, 1))
+    N.check(N.lib.glfsx_shard_device(block_size, salt, cid_key, d_range, size,
+                                     first_block, nb, d_ctext, out, stream))
+    return out.raw[:64 * m]
+
+
+def root_from_level1(N, block_size: int, salt, cid_key, level1: bytes, size: int):
+    r = N.glfsx_root()
+    N.check(N.lib.glfsx_root_from_level1(block_size, salt, cid_key, level1,
+                                         len(level1) // 64, size, ctypes.byref(r)))
+    return bytes(r.ref)
