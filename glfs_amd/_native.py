@@ -78,6 +78,10 @@ SIGNATURES = {
                                   _VP, _VP]),
     "glfsx_root_from_level1": (_INT, [_U64, _CP, _CP, _CP, _U64, _U64,
                                       ctypes.POINTER(glfsx_root)]),
+    "glfsx_post_blobs": (_INT, [_U64, _U64, _CP, _CP, _VP, _VP, _VP, _U64, POST_FN, _VP,
+                                _VP]),
+    "glfsx_post_blobs_device": (_INT, [_U64, _CP, _CP, _VP, _VP, _VP, _U64, _U64, _VP,
+                                       _VP, _VP]),
     "glfsx_chacha20_xor": (_INT, [_CP, _VP, _VP, _U64]),
     "glfsx_fill_splitmix_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
     "glfsx_depth": (_INT, [_U64, _U64]),

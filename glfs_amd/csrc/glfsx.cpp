@@ -174,12 +174,31 @@ struct Salts {
   uint8_t raw[32], index[32];
 };
 
-// blob.go:99-101
+// blob.go:99-101.  DeriveKey is a pure function, so the (salt -> indexSalt,
+// rawSalt) pairs are memoised per thread: NewWriter is called once per blob by
+// glfs.PostBlob (machine.go:64) and would otherwise cost two launches each.
+struct SaltCacheEntry {
+  uint8_t salt[32];
+  Salts s;
+};
+thread_local std::vector<SaltCacheEntry> tls_salts;
+
 int derive_salts(Ctx *c, const uint8_t *salt, Salts *s) {
   static const uint8_t zero[32] = {0};
   const uint8_t *sl = salt ? salt : zero;
+  for (const auto &e : tls_salts)
+    if (memcmp(e.salt, sl, 32) == 0) {
+      *s = e.s;
+      return 0;
+    }
   if (int e = derive_key_dev(c, s->index, sl, "index", 5)) return e;
-  return derive_key_dev(c, s->raw, sl, "raw", 3);
+  if (int e = derive_key_dev(c, s->raw, sl, "raw", 3)) return e;
+  if (tls_salts.size() >= 64) tls_salts.erase(tls_salts.begin());
+  SaltCacheEntry ent;
+  memcpy(ent.salt, sl, 32);
+  ent.s = *s;
+  tls_salts.push_back(ent);
+  return 0;
 }
 
 // Post `nodes` index nodes (each exactly bs bytes) starting at d_nodes;
@@ -796,6 +815,95 @@ int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
   HIP_TRY(launch_chacha_xor(k, c->d_in.u8(), c->d_ct.u8(), n, c->stream));
   HIP_TRY(hipMemcpyAsync(dst, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
+                            const uint8_t *cid_key, const void *d_data,
+                            const uint64_t *d_offsets, const uint64_t *d_lengths,
+                            uint64_t n, uint64_t max_len, void *d_ctext,
+                            void *d_roots, void *stream) {
+  if (n == 0) return 0;
+  if (!d_data || !d_offsets || !d_lengths || !d_roots)
+    return fail(GLFSX_E_ARG, "null argument");
+  if (int e = check_block_size(block_size)) return e;
+  if (max_len > block_size)
+    return fail(GLFSX_E_ARG, "blob of %llu bytes spans more than one %llu-byte block",
+                (unsigned long long)max_len, (unsigned long long)block_size);
+  if (max_len > kMaxSmallLen)
+    return fail(GLFSX_E_UNSUPPORTED, "small-blob kernel limited to %llu bytes",
+                (unsigned long long)kMaxSmallLen);
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  SmallJob j{};
+  j.src = static_cast<const uint8_t *>(d_data);
+  j.ctext = static_cast<uint8_t *>(d_ctext);
+  j.offs = d_offsets;
+  j.lens = d_lengths;
+  j.n = n;
+  j.max_len = max_len;
+  j.refs = static_cast<uint8_t *>(d_roots);
+  words_from_key(j.raw_salt, salts.raw);
+  words_from_key(j.index_salt, salts.index);
+  if (cid_key) {
+    words_from_key(j.cid_key, cid_key);
+    j.cid_keyed = true;
+  } else {
+    blake3_iv_words(j.cid_key);
+  }
+  HIP_TRY(launch_post_small(j, pick_stream(c, stream)));
+  return 0;
+}
+
+int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
+                     const uint8_t *cid_key, const void *data,
+                     const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
+                     glfsx_post_fn post, void *post_ctx, uint8_t *roots_out) {
+  if (n == 0) return 0;
+  if (!data || !offsets || !lengths || !roots_out)
+    return fail(GLFSX_E_ARG, "null argument");
+  const uint64_t bs = block_size ? block_size : store_max;  // blob.go:86-89
+  if (bs > store_max)
+    return fail(GLFSX_E_BLOCKSIZE_GT_MAX, "blockSize %llu > maxSize %llu",
+                (unsigned long long)bs, (unsigned long long)store_max);
+  if (int e = check_block_size(bs)) return e;
+  uint64_t span = 0, max_len = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    span = std::max(span, offsets[i] + lengths[i]);
+    max_len = std::max(max_len, lengths[i]);
+  }
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  if (int e = c->d_in.ensure(span + 64)) return e;
+  if (int e = c->d_ct.ensure(span + 64)) return e;
+  if (int e = c->d_refs.ensure(64 * n)) return e;
+  if (int e = c->d_lvl_a.ensure(16 * n)) return e;
+  std::vector<uint8_t> h_ct(post ? span + 1 : 0);
+  uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_lvl_a.p);
+  uint64_t *d_len = d_off + n;
+  HIP_TRY(hipMemcpyAsync(c->d_in.p, data, span, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_off, offsets, 8 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_len, lengths, 8 * n, hipMemcpyHostToDevice, c->stream));
+  if (int e = glfsx_post_blobs_device(bs, salt, cid_key, c->d_in.p, d_off, d_len, n,
+                                      max_len, c->d_ct.p, c->d_refs.p, c->stream))
+    return e;
+  HIP_TRY(hipMemcpyAsync(roots_out, c->d_refs.p, 64 * n, hipMemcpyDeviceToHost,
+                         c->stream));
+  if (post && span)
+    HIP_TRY(hipMemcpyAsync(h_ct.data(), c->d_ct.p, span, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (post) {
+    for (uint64_t i = 0; i < n; ++i) {
+      // one PostBlob per blob, in order: its single Post (a data block, or
+      // the empty index node, blob.go:187-189)
+      int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
+                    h_ct.data() + offsets[i], lengths[i]);
+      if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+    }
+  }
   return 0;
 }
 

@@ -50,6 +50,21 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
 hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
                              uint8_t *dst, uint64_t n, hipStream_t s);
 
+// Many small blobs, one lane each (glfs.PostBlob batched): blob i is
+// src[offs[i] .. offs[i]+lens[i]), 0 <= lens[i] <= kMaxSmallLen; its root ref
+// (CID || DEK) goes to refs + 64*i.  Empty blobs use index_salt.
+constexpr uint64_t kMaxSmallLen = 16ull * 1024;
+struct SmallJob {
+  const uint8_t *src;
+  uint8_t *ctext;  // nullable; same offsets as src
+  const uint64_t *offs, *lens;  // device arrays
+  uint64_t n, max_len;
+  uint8_t *refs;
+  uint32_t raw_salt[8], index_salt[8], cid_key[8];
+  bool cid_keyed;
+};
+hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
+
 // Synthetic splitmix64 byte stream (see oracle_fill_splitmix); offset % 8 == 0.
 hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
                        hipStream_t s);

@@ -251,59 +251,75 @@ __device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
   }
 }
 
+// One full 64-B block of the fast path: (ChaCha20 keystream XOR, ctext
+// store,) BLAKE3 compression.
+template <bool CHACHA>
+__device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
+                                           const uint4 &w1, const uint4 &w2,
+                                           const uint4 &w3, uint32_t chunk,
+                                           uint32_t b, uint32_t fl,
+                                           const uint32_t (&dek)[8],
+                                           uint4 *out) {
+  uint32_t m[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                    w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+  if constexpr (CHACHA) {
+    uint32_t x[16];
+    chacha_block(x, dek, (chunk << 4) + b);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+    if (out) {
+      out[0] = make_uint4(m[0], m[1], m[2], m[3]);
+      out[1] = make_uint4(m[4], m[5], m[6], m[7]);
+      out[2] = make_uint4(m[8], m[9], m[10], m[11]);
+      out[3] = make_uint4(m[12], m[13], m[14], m[15]);
+    }
+  }
+  b3_compress(cv, m, chunk, 0u, 64u, fl);
+}
+
 // Fast path: the lane's G chunks are all full (16*G consecutive 64-B blocks,
-// 16-B aligned).  One loop over the blocks with the next block's four 16-B
-// loads issued before the current compression, so the wave does not stall
-// on HBM latency between blocks.
+// 16-B aligned).  Blocks go in pairs through two named register buffers: the
+// odd block's loads are issued before the even block is compressed and the
+// next even block's before the odd one, so HBM latency is covered and no
+// buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
+// the chaining-value reset are per-chunk (scalar), not per-block selects.
 template <int G, bool CHACHA>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
     const uint32_t (&dek)[8]) {
   constexpr int D = ilog2(G);
+  constexpr uint32_t NB = 16u * G;
   uint32_t stk[D > 0 ? D : 1][8];
   uint32_t depth = 0;
   const uint4 *q = reinterpret_cast<const uint4 *>(msg + (uint64_t(first) << 10));
   uint4 *cq = cmsg ? reinterpret_cast<uint4 *>(cmsg + (uint64_t(first) << 10))
                    : nullptr;
-  uint4 n0 = q[0], n1 = q[1], n2 = q[2], n3 = q[3];
-  for (uint32_t blk = 0; blk < 16u * G; ++blk) {
-    uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w,
-                      n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
-    if (blk + 1 < 16u * G) {
-      const uint4 *nq = q + 4 * (blk + 1);
-      n0 = nq[0];
-      n1 = nq[1];
-      n2 = nq[2];
-      n3 = nq[3];
-    }
-    const uint32_t b = blk & 15u, jj = blk >> 4;
+  uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
     const uint32_t chunk = first + jj;
-    if (b == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) cv[i] = key[i];
-    }
-    if constexpr (CHACHA) {
-      uint32_t x[16];
-      chacha_block(x, dek, (chunk << 4) + b);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] ^= x[i];
-      if (cq) {
-        uint4 *o = cq + 4 * blk;
-        o[0] = make_uint4(m[0], m[1], m[2], m[3]);
-        o[1] = make_uint4(m[4], m[5], m[6], m[7]);
-        o[2] = make_uint4(m[8], m[9], m[10], m[11]);
-        o[3] = make_uint4(m[12], m[13], m[14], m[15]);
+    for (int i = 0; i < 8; ++i) cv[i] = key[i];
+    for (uint32_t pp = 0; pp < 8; ++pp) {
+      const uint32_t blk = jj * 16 + 2 * pp;
+      const uint4 *nb = q + 4 * (blk + 1);
+      uint4 b0 = nb[0], b1 = nb[1], b2 = nb[2], b3 = nb[3];
+      full_block<CHACHA>(cv, a0, a1, a2, a3, chunk, 2 * pp,
+                         base | (pp == 0 ? kChunkStart : 0u), dek,
+                         cq ? cq + 4 * blk : nullptr);
+      if (blk + 2 < NB) {
+        const uint4 *na = q + 4 * (blk + 2);
+        a0 = na[0];
+        a1 = na[1];
+        a2 = na[2];
+        a3 = na[3];
       }
+      uint32_t fl = base;
+      if (pp == 7) fl |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
+      full_block<CHACHA>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
+                         cq ? cq + 4 * (blk + 1) : nullptr);
     }
-    uint32_t fl = base;
-    if (b == 0) fl |= kChunkStart;
-    if (b == 15) {
-      fl |= kChunkEnd;
-      if (whole && G == 1) fl |= kRoot;
-    }
-    b3_compress(cv, m, chunk, 0u, 64u, fl);
-    if (b == 15) lane_merge<D>(cv, stk, depth, jj, jj + 1 == G, whole, key, base);
+    lane_merge<D>(cv, stk, depth, jj, jj + 1 == uint32_t(G), whole, key, base);
   }
 }
 
@@ -456,6 +472,56 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   }
 }
 
+// Small blobs (glfs.PostBlob of many blobs that each fit one bigblob block,
+// e.g. BASELINE config 4's 1M x 4 KiB): one lane per blob.  A blob of
+// 0 < len <= block_size has root = post(rawSalt, blob) (blob.go:190-193); the
+// empty blob has root = post(indexSalt, "") (blob.go:187-189), so the key is
+// selected per lane.  Every lane finishes its own BLAKE3 tree (G >= chunks).
+struct SArgs {
+  const uint8_t *src;
+  uint8_t *ctext;
+  const uint64_t *offs;
+  const uint64_t *lens;
+  uint64_t n;
+  uint8_t *refs;      // 64 B per blob, dense
+  uint32_t key[8];    // DEK pass: rawSalt words; CID pass: CID key words
+  uint32_t key0[8];   // DEK pass: indexSalt words (empty blobs); CID pass: = key
+  uint32_t base;
+  uint32_t out_off;
+};
+
+template <int G, bool CHACHA>
+__global__ __launch_bounds__(256) void k_small(SArgs a) {
+  const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  if (i >= a.n) return;  // no barriers in this kernel
+  const uint64_t off = a.offs[i], len = a.lens[i];
+  const uint8_t *msg = a.src + off;
+  uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + off : nullptr;
+  uint8_t *ref = a.refs + i * 64;
+  uint32_t key[8], dek[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) key[w] = len ? a.key[w] : a.key0[w];
+  if constexpr (CHACHA) {
+    const uint32_t *dp = reinterpret_cast<const uint32_t *>(ref + 32);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) dek[w] = dp[w];
+  } else {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) dek[w] = 0;
+  }
+  const uint32_t C = len ? uint32_t((len + 1023) >> 10) : 1u;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(msg) |
+                         reinterpret_cast<uintptr_t>(cmsg)) & 15) == 0;
+  uint32_t cv[8];
+  if (aligned && len == uint64_t(G) << 10)
+    lane_subtree_full<G, CHACHA>(cv, msg, cmsg, 0u, true, key, a.base, dek);
+  else if (aligned)
+    lane_subtree<G, CHACHA, true>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
+  else
+    lane_subtree<G, CHACHA, false>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
+  store_digest(ref + a.out_off, cv);
+}
+
 __global__ __launch_bounds__(256) void k_chacha_xor(KArgs a) {
   uint32_t k[8];
 #pragma unroll
@@ -531,6 +597,21 @@ hipError_t launch_pass(const KArgs &a, uint64_t maxlen, bool aligned,
   }
 }
 
+template <bool CHACHA>
+hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
+  const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
+  const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
+  switch (C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0) {
+    case 1: hipLaunchKernelGGL((k_small<1, CHACHA>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_small<2, CHACHA>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_small<4, CHACHA>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_small<8, CHACHA>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_small<16, CHACHA>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 KArgs make_args(const PostJob &job) {
   KArgs a{};
   a.src = job.src;
@@ -604,6 +685,30 @@ hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
   hipLaunchKernelGGL(k_fill, dim3(uint32_t(grid)), dim3(256), 0, s, dst, offset,
                      n, seed);
   return hipGetLastError();
+}
+
+hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
+  if (job.n == 0) return hipSuccess;
+  if (job.max_len > kMaxSmallLen) return hipErrorInvalidValue;
+  SArgs a{};
+  a.src = job.src;
+  a.ctext = job.ctext;
+  a.offs = job.offs;
+  a.lens = job.lens;
+  a.n = job.n;
+  a.refs = job.refs;
+  for (int i = 0; i < 8; ++i) {
+    a.key[i] = job.raw_salt[i];
+    a.key0[i] = job.index_salt[i];
+  }
+  a.base = kKeyed;
+  a.out_off = 32;
+  hipError_t e = launch_small_pass<false>(a, job.max_len, s);
+  if (e != hipSuccess) return e;
+  for (int i = 0; i < 8; ++i) a.key[i] = a.key0[i] = job.cid_key[i];
+  a.base = job.cid_keyed ? kKeyed : 0u;
+  a.out_off = 0;
+  return launch_small_pass<true>(a, job.max_len, s);
 }
 
 hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,

@@ -86,6 +86,35 @@ class Machine:
         """blob.go:15-17."""
         return self.post_typed(store, TYPE_BLOB, r)
 
+    def post_blobs(self, store, blobs) -> list:
+        """n sequential PostBlob calls (machine.go:64-66) for blobs that each
+        fit one block, batched into one GPU launch pair (one lane per blob).
+        The store sees the same Posts in the same order."""
+        import ctypes
+        from . import _native as N
+        blobs = [bytes(b) for b in blobs]
+        n = len(blobs)
+        if n == 0:
+            return []
+        offs, lens, pos = [], [], 0
+        for b in blobs:
+            offs.append(pos)
+            lens.append(len(b))
+            pos += len(b)
+        data = b"".join(blobs)
+        O = (ctypes.c_uint64 * n)(*offs)
+        L = (ctypes.c_uint64 * n)(*lens)
+        roots = ctypes.create_string_buffer(64 * n)
+        cb, errors = bigblob._make_post_cb(store)
+        rc = N.lib.glfsx_post_blobs(self.block_size, store.max_size(),
+                                    self.make_salt(TYPE_BLOB), None, data or b"\0",
+                                    O, L, n, cb, None, roots)
+        if rc == N.GLFSX_E_STORE and errors:
+            raise bigblob.StoreError(rc, repr(errors[0])) from errors[0]
+        N.check(rc)
+        return [Ref(TYPE_BLOB, Root(bigblob.Ref.from_bytes(roots.raw[64 * i:64 * i + 64]),
+                                    lens[i], self.block_size)) for i in range(n)]
+
     def new_blob_writer(self, store) -> TypedWriter:
         """blob.go:37-39."""
         return self.new_typed_writer(store, TYPE_BLOB)
@@ -109,3 +138,8 @@ def post_typed(store, ty: str, r) -> Ref:
 def post_blob(store, r) -> Ref:
     """machine.go:64-66."""
     return _default_machine().post_blob(store, r)
+
+
+def post_blobs(store, blobs) -> list:
+    """Batched PostBlob on the default machine (see Machine.post_blobs)."""
+    return _default_machine().post_blobs(store, blobs)

@@ -20,6 +20,8 @@
  *   glfsx_create_device    Create over a device-resident blob (no host copies)
  *   glfsx_shard_device /   the same, split by disjoint block ranges across
  *   glfsx_root_from_level1 GPUs; the caller gathers the level-1 refs
+ *   glfsx_post_blobs*      glfs machine.go:64 PostBlob, batched over many
+ *                          single-block blobs (tree.go:300-316 callers)
  *   glfsx_depth            bigblob/blob.go:256-264 depth()
  *   glfsx_chacha20_xor*    bigblob/ref.go:137-144  cryptoXOR (read side decrypt)
  *
@@ -157,6 +159,26 @@ int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
 int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
                            const uint8_t *cid_key, const uint8_t *level1,
                            uint64_t n1, uint64_t size, glfsx_root *out);
+
+/* --- many small blobs (glfs.PostBlob batched; BASELINE config 4) -------- */
+/* Blob i is data[offsets[i] .. offsets[i]+lengths[i]).  Every blob must fit
+ * one bigblob block (0 <= len <= block_size; this kernel family also caps
+ * len at 16 KiB), so its root is post(rawSalt, blob) (blob.go:190-193) or,
+ * for an empty blob, post(indexSalt, "") (blob.go:187-189); rawSalt /
+ * indexSalt derive from `salt` (glfs: the type salt, machine.go:50-54).
+ * Writes 64-byte root refs (CID||DEK) per blob.  The host variant calls
+ * `post` once per blob in order, like n sequential PostBlob calls. */
+int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
+                     const uint8_t *cid_key, const void *data,
+                     const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
+                     glfsx_post_fn post, void *post_ctx, uint8_t *roots_out);
+/* Device-resident: d_offsets / d_lengths are device arrays; max_len is the
+ * largest length (caller-known).  Enqueued on stream, not synchronised. */
+int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
+                            const uint8_t *cid_key, const void *d_data,
+                            const uint64_t *d_offsets, const uint64_t *d_lengths,
+                            uint64_t n, uint64_t max_len, void *d_ctext,
+                            void *d_roots, void *stream);
 
 /* --- read side (ref.go:113-126 getF decrypt) ---------- */
 /* ChaCha20, zero nonce, counter 0, key = dek (ref.go:137-144). */

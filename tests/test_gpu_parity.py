@@ -364,3 +364,49 @@ def test_large_blob_properties(gpu, O):
                                           refs.data_ptr(), None, None))
     torch.cuda.synchronize()
     assert host(refs, 64 * n0) == rh
+
+
+# ------------------------------------------------------------- small blobs
+def test_post_blobs_vs_oracle(gpu, O):
+    """Batched glfs.PostBlob (config 4 shape): every root, every Post, in order,
+    equal to n sequential reference PostBlob calls; empty and ragged blobs,
+    packed at unaligned offsets."""
+    from glfs_amd import bigblob, glfs
+    rng = random.Random(11)
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    lens = [0, 1, 9, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 8192, 16384]
+    lens += [rng.randrange(0, 16385) for _ in range(200)] + [4096] * 300
+    blobs = [O.fill_splitmix(n, 1000 + i) for i, n in enumerate(lens)]
+    store = bigblob.MemStore(2 << 20)
+    refs = glfs.Machine().post_blobs(store, blobs)
+    assert len(store.log) == len(blobs)
+    for i, (b, r) in enumerate(zip(blobs, refs)):
+        want, size, bs, posts = O.create(b, 2 << 20, salt=blob_salt)
+        assert r.root.ref.marshal_binary() == want, (i, len(b))
+        assert (r.root.size, r.root.block_size, r.type) == (len(b), 2 << 20, "blob")
+        assert store.log[i][:2] == (posts[0][0], posts[0][1])
+        assert store.blobs[want[:32]] == posts[0][3]
+
+
+def test_post_blobs_device_config4_sample(gpu, O):
+    """Config 4 shape on device: 65536 x 4 KiB distinct blobs (splitmix seed =
+    blob index region); sampled roots vs the oracle."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    n, ln = 65536, 4096
+    t = dev_bytes(torch, n * ln, seed=4)
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * ln
+    lens = torch.full((n,), ln, dtype=torch.int64, device="cuda")
+    roots = zeros(torch, 64 * n)
+    ct = zeros(torch, n * ln)
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    N.check(N.lib.glfsx_post_blobs_device(2 << 20, blob_salt, None, t.data_ptr(),
+                                          offs.data_ptr(), lens.data_ptr(), n, ln,
+                                          ct.data_ptr(), roots.data_ptr(), None))
+    torch.cuda.synchronize()
+    rh = host(roots, 64 * n)
+    data = host(t, n * ln)
+    rng = random.Random(5)
+    for i in [0, 1, n - 1] + rng.sample(range(n), 20):
+        want = O.create(data[i * ln:(i + 1) * ln], 2 << 20, salt=blob_salt)[0]
+        assert rh[64 * i:64 * i + 64] == want, i
