@@ -84,6 +84,8 @@ SIGNATURES = {
                                        _VP, _VP]),
     "glfsx_chacha20_xor": (_INT, [_CP, _VP, _VP, _U64]),
     "glfsx_fill_splitmix_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
+    "glfsx_decrypt_batch_device": (_INT, [_VP, _U64, _U64, _VP, _VP, _VP]),
+    "glfsx_sink_count": (_INT, [_VP, _INT, _VP, _VP, _U64]),
     "glfsx_depth": (_INT, [_U64, _U64]),
     "glfsx_branching_factor": (_U64, [_U64]),
 }

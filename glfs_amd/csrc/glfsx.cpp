@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/glfsx.h"
@@ -254,11 +255,26 @@ int build_up(Ctx *c, hipStream_t s, const Salts &salts, const uint8_t *cid_key,
 }  // namespace
 
 // ------------------------------------------------------------------ Writer
-// bigblob/blob.go:71-83.  Data blocks are staged in a pinned batch and hashed
-// on the GPU together; Post calls and index bookkeeping then replay the
+// bigblob/blob.go:71-83.  Complete blocks are staged in pinned batches and
+// hashed on the GPU; Post calls and index bookkeeping then replay the
 // reference's exact order (postBuf -> addRef -> maybe post index node).
+//
+// Two batch slots make the host round trip a pipeline: while batch k's H2D
+// copy, kernels and D2H copies run on the writer's stream, the caller's
+// Write()s fill batch k+1; batch k is completed (Posts delivered) when batch
+// k+1 is submitted or at Finish.
+struct WSlot {
+  PinBuf h_in;   // complete blocks (+ the block being filled while current)
+  PinBuf h_ct, h_refs;
+  DevBuf d_in, d_ct, d_refs;
+  hipEvent_t done = nullptr;
+  uint64_t nblk = 0;  // blocks in flight
+  bool busy = false;
+};
+
 struct glfsx_writer {
   Ctx *c = nullptr;
+  hipStream_t ws = nullptr;  // batch stream (post_one uses the thread's)
   uint64_t bs = 0, bf = 0;
   Salts salts{};
   uint8_t cid_key[32]{};
@@ -268,15 +284,13 @@ struct glfsx_writer {
   std::vector<std::vector<uint8_t>> indexes;  // index.go Index per level
   std::vector<uint64_t> counts;
   uint64_t size = 0;
-  // batch staging
-  PinBuf h_in, h_ct, h_refs;
-  PinBuf h_one;  // ctext of single posts (index nodes, the tail block): must
-                 // not alias h_ct, which flush() is still handing to the sink
-  DevBuf d_in;  // per-writer so concurrent writers on one thread don't clash
+  PinBuf h_one;  // ctext of single posts (index nodes, the tail block)
+  WSlot slot[2];
+  int cur = 0;               // slot being filled
   uint64_t batch_blocks = 1;
-  uint64_t full = 0;     // complete blocks staged
-  uint64_t partial = 0;  // bytes of the block being filled
-  int sticky = 0;        // first error; the writer is dead afterwards
+  uint64_t full = 0;         // complete blocks staged in slot[cur]
+  uint64_t partial = 0;      // bytes of the block being filled
+  int sticky = 0;            // first error; the writer is dead afterwards
 };
 
 namespace {
@@ -285,7 +299,44 @@ const uint8_t *cidk(const glfsx_writer *w) {
   return w->has_cid_key ? w->cid_key : nullptr;
 }
 
-// Post one message from host memory (ref.go:98 post + sink), synchronously.
+// Grow a pinned buffer keeping its first `keep` bytes.
+int pin_grow(PinBuf &b, size_t need, size_t keep) {
+  if (need <= b.cap) return 0;
+  size_t want = std::max(need, b.cap * 2);
+  void *p = nullptr;
+  HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+  if (b.p) {
+    if (keep) memcpy(p, b.p, keep);
+    (void)hipHostFree(b.p);
+  }
+  b.p = p;
+  b.cap = want;
+  return 0;
+}
+
+// Host copy into pinned staging; large copies are split over threads (the
+// Writer's memcpy into w.buf, blob.go:121-126, is its host-side cost).
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
+  constexpr size_t kMin = 8u << 20;
+  unsigned hw = std::thread::hardware_concurrency();
+  unsigned t = unsigned(std::min<size_t>(std::min(8u, hw ? hw : 1u), n / kMin));
+  if (t <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n / t + 4095) & ~size_t(4095);
+  for (unsigned i = 0; i < t; ++i) {
+    const size_t o = i * per;
+    if (o >= n) break;
+    const size_t k = std::min(per, n - o);
+    th.emplace_back([=] { memcpy(dst + o, src + o, k); });
+  }
+  for (auto &x : th) x.join();
+}
+
+// Post one message from host memory (ref.go:98 post + sink), synchronously,
+// on the thread's stream.
 int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
              const uint8_t *data, uint64_t n, uint8_t ref[64]) {
   Ctx *c = w->c;
@@ -338,47 +389,62 @@ int add_ref(glfsx_writer *w, size_t i, const uint8_t ref[64]) {
   return add_ref(w, i + 1, r2);
 }
 
-// Hash the staged complete blocks on the GPU, then replay postBuf for each
-// (blob.go:152-163) in order.
-int flush(glfsx_writer *w) {
-  if (w->full == 0) return 0;
-  Ctx *c = w->c;
-  const uint64_t nbytes = w->full * w->bs;
-  if (int e = w->d_in.ensure(nbytes)) return e;
-  if (int e = c->d_ct.ensure(nbytes)) return e;
-  if (int e = c->d_refs.ensure(w->full * 64)) return e;
-  if (int e = w->h_ct.ensure(nbytes + 64)) return e;
-  if (int e = w->h_refs.ensure(w->full * 64)) return e;
-  HIP_TRY(hipMemcpyAsync(w->d_in.p, w->h_in.p, nbytes, hipMemcpyHostToDevice,
-                         c->stream));
-  PostJob j{};
-  j.src = w->d_in.u8();
-  j.ctext = c->d_ct.u8();
-  j.stride = w->bs;
-  j.msg_len = w->bs;
-  j.last_len = w->bs;
-  j.n = w->full;
-  j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
-  words_from_key(j.salt, w->salts.raw);
-  cid_words(j, cidk(w));
-  HIP_TRY(launch_post(j, c->stream));
-  HIP_TRY(hipMemcpyAsync(w->h_refs.p, c->d_refs.p, w->full * 64,
-                         hipMemcpyDeviceToHost, c->stream));
-  if (w->post)
-    HIP_TRY(hipMemcpyAsync(w->h_ct.p, c->d_ct.p, nbytes, hipMemcpyDeviceToHost,
-                           c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  for (uint64_t b = 0; b < w->full; ++b) {
-    const uint8_t *ref = w->h_refs.u8() + 64 * b;
+// Wait for an in-flight batch and replay postBuf (blob.go:152-163) for each
+// of its blocks, in order.
+int complete(glfsx_writer *w, WSlot &sl) {
+  if (!sl.busy) return 0;
+  sl.busy = false;
+  HIP_TRY(hipEventSynchronize(sl.done));
+  for (uint64_t b = 0; b < sl.nblk; ++b) {
+    const uint8_t *ref = sl.h_refs.u8() + 64 * b;
     if (w->post) {
-      int rc = w->post(w->post_ctx, 0, ref, w->h_ct.u8() + b * w->bs, w->bs);
+      int rc = w->post(w->post_ctx, 0, ref, sl.h_ct.u8() + b * w->bs, w->bs);
       if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
     }
     if (int e = add_ref(w, 0, ref)) return e;
     w->size += w->bs;
   }
-  if (w->partial)
-    memmove(w->h_in.u8(), w->h_in.u8() + nbytes, w->partial);
+  return 0;
+}
+
+// Enqueue the current slot's complete blocks (H2D, DEK + ChaCha/CID kernels,
+// D2H of refs and ctext), finish the other slot's batch, and switch slots,
+// carrying the partially filled block over.
+int submit(glfsx_writer *w) {
+  if (w->full == 0) return 0;
+  WSlot &sl = w->slot[w->cur];
+  WSlot &nx = w->slot[w->cur ^ 1];
+  const uint64_t nbytes = w->full * w->bs;
+  if (int e = sl.d_in.ensure(nbytes)) return e;
+  if (int e = sl.d_ct.ensure(nbytes)) return e;
+  if (int e = sl.d_refs.ensure(w->full * 64)) return e;
+  if (w->post)
+    if (int e = sl.h_ct.ensure(nbytes + 64)) return e;
+  if (int e = sl.h_refs.ensure(w->full * 64)) return e;
+  if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->ws));
+  PostJob j{};
+  j.src = sl.d_in.u8();
+  j.ctext = sl.d_ct.u8();
+  j.stride = w->bs;
+  j.msg_len = w->bs;
+  j.last_len = w->bs;
+  j.n = w->full;
+  j.out = RefLayout{sl.d_refs.u8(), ~0ull, 0};
+  words_from_key(j.salt, w->salts.raw);
+  cid_words(j, cidk(w));
+  HIP_TRY(launch_post(j, w->ws));
+  HIP_TRY(hipMemcpyAsync(sl.h_refs.p, sl.d_refs.p, w->full * 64,
+                         hipMemcpyDeviceToHost, w->ws));
+  if (w->post)
+    HIP_TRY(hipMemcpyAsync(sl.h_ct.p, sl.d_ct.p, nbytes, hipMemcpyDeviceToHost, w->ws));
+  HIP_TRY(hipEventRecord(sl.done, w->ws));
+  sl.nblk = w->full;
+  sl.busy = true;
+  if (int e = complete(w, nx)) return e;  // the previous batch, in order
+  if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
+  if (w->partial) memcpy(nx.h_in.u8(), sl.h_in.u8() + nbytes, w->partial);
+  w->cur ^= 1;
   w->full = 0;
   return 0;
 }
@@ -593,31 +659,35 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   w->indexes.emplace_back(bs, 0);  // blob.go:111
   w->counts.push_back(0);
   w->batch_blocks = std::max<uint64_t>(1, (64ull << 20) / bs);
+  if (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess) {
+    delete w;
+    *err = fail(GLFSX_E_DEVICE, "hipStreamCreate failed");
+    return nullptr;
+  }
   *err = 0;
   return w;
 }
 
 // blob.go:120-133: a block is complete exactly when buffered + incoming
-// reaches bs; it is staged and hashed with the rest of its batch.
+// reaches bs; complete blocks are hashed a batch at a time.
 int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
   if (!w) return fail(GLFSX_E_ARG, "null writer");
   if (w->sticky) return w->sticky;
   if (n && !data) return fail(GLFSX_E_ARG, "null data");
   const uint8_t *p = static_cast<const uint8_t *>(data);
-  if (int e = w->h_in.ensure((w->batch_blocks + 1) * w->bs)) return w->sticky = e;
   while (n) {
-    const uint64_t room = w->bs - w->partial;
-    const uint64_t take = std::min<uint64_t>(room, n);
-    memcpy(w->h_in.u8() + w->full * w->bs + w->partial, p, take);
-    w->partial += take;
+    WSlot &sl = w->slot[w->cur];
+    const uint64_t used = w->full * w->bs + w->partial;
+    const uint64_t cap = w->batch_blocks * w->bs;  // slot holds up to a batch
+    const uint64_t take = std::min<uint64_t>(cap - used, n);
+    if (int e = pin_grow(sl.h_in, used + take, used)) return w->sticky = e;
+    par_memcpy(sl.h_in.u8() + used, p, take);
     p += take;
     n -= take;
-    if (w->partial == w->bs) {
-      w->full++;
-      w->partial = 0;
-      if (w->full == w->batch_blocks)
-        if (int e = flush(w)) return w->sticky = e;
-    }
+    w->full = (used + take) / w->bs;
+    w->partial = (used + take) % w->bs;
+    if (w->full == w->batch_blocks)
+      if (int e = submit(w)) return w->sticky = e;
   }
   return 0;
 }
@@ -625,10 +695,12 @@ int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
 int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   if (!w || !out) return fail(GLFSX_E_ARG, "null argument");
   if (w->sticky) return w->sticky;
-  if (int e = flush(w)) return w->sticky = e;
+  if (int e = submit(w)) return w->sticky = e;
+  for (int k = 0; k < 2; ++k)  // at most one batch is still in flight
+    if (int e = complete(w, w->slot[w->cur ^ 1 ^ k])) return w->sticky = e;
   if (w->partial) {  // blob.go:136-140: the tail block, never padded
     uint8_t ref[64];
-    if (int e = post_one(w, 0, w->salts.raw, w->h_in.u8(), w->partial, ref))
+    if (int e = post_one(w, 0, w->salts.raw, w->slot[w->cur].h_in.u8(), w->partial, ref))
       return w->sticky = e;
     if (int e = add_ref(w, 0, ref)) return w->sticky = e;
     w->size += w->partial;
@@ -644,11 +716,18 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
 
 void glfsx_writer_free(glfsx_writer *w) {
   if (!w) return;
-  if (w->h_in.p) (void)hipHostFree(w->h_in.p);
-  if (w->h_ct.p) (void)hipHostFree(w->h_ct.p);
-  if (w->h_refs.p) (void)hipHostFree(w->h_refs.p);
+  if (w->ws) (void)hipStreamSynchronize(w->ws);
+  for (auto &sl : w->slot) {
+    if (sl.h_in.p) (void)hipHostFree(sl.h_in.p);
+    if (sl.h_ct.p) (void)hipHostFree(sl.h_ct.p);
+    if (sl.h_refs.p) (void)hipHostFree(sl.h_refs.p);
+    if (sl.d_in.p) (void)hipFree(sl.d_in.p);
+    if (sl.d_ct.p) (void)hipFree(sl.d_ct.p);
+    if (sl.d_refs.p) (void)hipFree(sl.d_refs.p);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
   if (w->h_one.p) (void)hipHostFree(w->h_one.p);
-  if (w->d_in.p) (void)hipFree(w->d_in.p);
+  if (w->ws) (void)hipStreamDestroy(w->ws);
   delete w;
 }
 
@@ -915,6 +994,38 @@ int glfsx_fill_splitmix_device(void *d_dst, uint64_t offset, uint64_t n,
   if (int e = ctx_get(&c)) return e;
   HIP_TRY(launch_fill(static_cast<uint8_t *>(d_dst), offset, n, seed,
                       pick_stream(c, stream)));
+  return 0;
+}
+
+int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
+                               uint64_t block_size, const void *d_refs,
+                               void *d_ptext, void *stream) {
+  if (total == 0) return 0;
+  if (!d_ctext || !d_refs || !d_ptext) return fail(GLFSX_E_ARG, "null argument");
+  if (block_size == 0 || block_size % 64)
+    return fail(GLFSX_E_UNSUPPORTED, "decrypt needs block_size %% 64 == 0");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  const uint64_t n = (total + block_size - 1) / block_size;
+  HIP_TRY(launch_decrypt(static_cast<const uint8_t *>(d_ctext),
+                         static_cast<uint8_t *>(d_ptext), n, block_size,
+                         total - (n - 1) * block_size,
+                         static_cast<const uint8_t *>(d_refs), pick_stream(c, stream)));
+  return 0;
+}
+
+// A store sink that only counts (benchmarks, tests): ctx -> uint64_t[2] =
+// {posts, bytes}.  Stands in for a native store's Post at ~zero cost.
+int glfsx_sink_count(void *ctx, int kind, const uint8_t *ref, const void *ctext,
+                     uint64_t len) {
+  (void)kind;
+  (void)ref;
+  (void)ctext;
+  uint64_t *c = static_cast<uint64_t *>(ctx);
+  if (c) {
+    c[0] += 1;
+    c[1] += len;
+  }
   return 0;
 }
 

@@ -65,6 +65,12 @@ struct SmallJob {
 };
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
 
+// Read side: decrypt n contiguous blocks (bs % 64 == 0; the last one
+// last_len bytes) with the DEKs in bytes [32,64) of refs[j] (dense).
+hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
+                          uint64_t bs, uint64_t last_len, const uint8_t *refs,
+                          hipStream_t s);
+
 // Synthetic splitmix64 byte stream (see oracle_fill_splitmix); offset % 8 == 0.
 hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
                        hipStream_t s);

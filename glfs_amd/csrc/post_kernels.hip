@@ -522,6 +522,36 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
   store_digest(ref + a.out_off, cv);
 }
 
+// Read side (bigblob/ref.go:113-126 getF -> cryptoXOR, blob.go:31-69): decrypt
+// n blocks of bs bytes (bs % 64 == 0) laid out contiguously, block j with
+// the DEK in bytes [32,64) of refs[j].  One thread per 64-B keystream block.
+__global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
+  const uint64_t per = a.msg_len >> 6;  // keystream blocks per bigblob block
+  const uint64_t total_kb = (a.n - 1) * per + ((a.last_len + 63) >> 6);
+  for (uint64_t kb = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; kb < total_kb;
+       kb += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t j = kb / per;
+    const uint32_t ctr = uint32_t(kb - j * per);
+    const uint64_t off = kb << 6;
+    const uint64_t end = j * a.msg_len + ((j + 1 == a.n) ? a.last_len : a.msg_len);
+    const uint32_t avail = uint32_t(min<uint64_t>(64, end - off));
+    const uint32_t *dp = reinterpret_cast<const uint32_t *>(a.refs + j * 64 + 32);
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = dp[i];
+    uint32_t m[16], x[16];
+    const bool al = ((reinterpret_cast<uintptr_t>(a.src) |
+                      reinterpret_cast<uintptr_t>(a.ctext)) & 15) == 0;
+    if (al) load_block<true>(m, a.src + off, avail);
+    else load_block<false>(m, a.src + off, avail);
+    chacha_block(x, k, ctr);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+    if (al) store_block<true>(a.ctext + off, m, avail);
+    else store_block<false>(a.ctext + off, m, avail);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_chacha_xor(KArgs a) {
   uint32_t k[8];
 #pragma unroll
@@ -709,6 +739,25 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;
   return launch_small_pass<true>(a, job.max_len, s);
+}
+
+hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
+                          uint64_t bs, uint64_t last_len, const uint8_t *refs,
+                          hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (bs % 64) return hipErrorInvalidValue;
+  KArgs a{};
+  a.src = ctext;
+  a.ctext = ptext;
+  a.msg_len = bs;
+  a.last_len = last_len;
+  a.n = n;
+  a.refs = const_cast<uint8_t *>(refs);
+  const uint64_t kbs = ((n - 1) * bs + last_len + 63) >> 6;
+  uint64_t grid = (kbs + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(k_decrypt, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,

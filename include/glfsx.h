@@ -193,6 +193,19 @@ int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
 int glfsx_fill_splitmix_device(void *d_dst, uint64_t offset, uint64_t n,
                                uint64_t seed, void *stream);
 
+/* A glfsx_post_fn that only counts: ctx points at uint64_t[2] = {posts,
+ * bytes}.  For benchmarks of the host round trip without a store. */
+int glfsx_sink_count(void *ctx, int kind, const uint8_t *ref, const void *ctext,
+                     uint64_t len);
+
+/* Batched getF decrypt (ref.go:113-126): block j of d_ctext (block_size
+ * bytes, the last one short; block_size % 64 == 0 as the reader requires,
+ * blob.go:59) is decrypted with the DEK in bytes [32,64) of the 64-byte ref
+ * j of d_refs into d_ptext.  Device pointers; enqueued on stream. */
+int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
+                               uint64_t block_size, const void *d_refs,
+                               void *d_ptext, void *stream);
+
 /* --- tree shape (blob.go:219-268) -------------------------------------- */
 int glfsx_depth(uint64_t size, uint64_t block_size);
 uint64_t glfsx_branching_factor(uint64_t block_size);

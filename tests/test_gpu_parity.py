@@ -410,3 +410,27 @@ def test_post_blobs_device_config4_sample(gpu, O):
     for i in [0, 1, n - 1] + rng.sample(range(n), 20):
         want = O.create(data[i * ln:(i + 1) * ln], 2 << 20, salt=blob_salt)[0]
         assert rh[64 * i:64 * i + 64] == want, i
+
+
+# ---------------------------------------------------------------- read side
+@pytest.mark.parametrize("bs,size", [(1 << 20, (9 << 20) + 77), (4096, 4096 * 33 + 5),
+                                     (128, 128 * 7)])
+def test_decrypt_batch_roundtrip(gpu, O, bs, size):
+    """getF (ref.go:113-126): decrypting every posted data block with its DEK
+    gives back the plaintext; block 0 also checked against the oracle."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    raw = O.derive_key(bytes(32), b"raw")
+    n = -(-size // bs)
+    t = dev_bytes(torch, size, seed=31)
+    ct = zeros(torch, size + 64)
+    refs = zeros(torch, 64 * n)
+    pt = zeros(torch, size + 64)
+    N.check(N.lib.glfsx_post_batch_device(raw, t.data_ptr(), size, bs, ct.data_ptr(),
+                                          refs.data_ptr(), None, None))
+    N.check(N.lib.glfsx_decrypt_batch_device(ct.data_ptr(), size, bs, refs.data_ptr(),
+                                             pt.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert torch.equal(pt[:size], t[:size])
+    r0 = host(refs, 64)
+    assert O.chacha20_xor(host(ct, min(bs, size)), r0[32:]) == host(t, min(bs, size))
