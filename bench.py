@@ -198,6 +198,23 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             times["dek"].append(e[0].elapsed_time(e[1]))
             times["cid"].append(e[1].elapsed_time(e[2]))
     avg = {k: sum(v[1:]) / reps for k, v in times.items()}  # first rep = warm-up
+    read = None
+    if ct is not None:
+        # read side (getF decrypt, ref.go:113-126): ctext -> ptext written over
+        # the plaintext buffer (identical bytes), DEKs from the refs above
+        tr = []
+        with torch.cuda.stream(stream):
+            for _ in range(reps + 1):
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record(stream)
+                N.check(N.lib.glfsx_decrypt_batch_device(ct, per, bs, refs.data_ptr(),
+                                                         data.data_ptr(), sp))
+                e[1].record(stream)
+                e[1].synchronize()
+                tr.append(e[0].elapsed_time(e[1]))
+        rms = sum(tr[1:]) / reps
+        read = {"value": round(per / GIB / (rms * 1e-3), 1), "unit": "GiB/s", "ms": round(rms, 3),
+                "what": "batched getF decrypt (ChaCha20 with each block's DEK), HBM->HBM"}
     alg = {"dek": per, "cid": per * (2 if ct is not None else 1)}
     dom = max(avg, key=avg.get)
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
@@ -222,6 +239,7 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             "frac": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 3)
                      for k in avg}}
     del refs
+    roof["read_side"] = read
     return roof, valu
 
 

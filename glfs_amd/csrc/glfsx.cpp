@@ -267,14 +267,19 @@ struct WSlot {
   PinBuf h_in;   // complete blocks (+ the block being filled while current)
   PinBuf h_ct, h_refs;
   DevBuf d_in, d_ct, d_refs;
-  hipEvent_t done = nullptr;
+  hipEvent_t up = nullptr, hashed = nullptr, done = nullptr;
   uint64_t nblk = 0;  // blocks in flight
+  uint64_t seq = 0;   // submission order
   bool busy = false;
 };
 
+constexpr int kSlots = 3;  // fill / upload+hash / download can all overlap
+
 struct glfsx_writer {
   Ctx *c = nullptr;
-  hipStream_t ws = nullptr;  // batch stream (post_one uses the thread's)
+  // batch streams (post_one uses the thread's): uploads, kernels, downloads,
+  // so batch k+1's H2D overlaps batch k's D2H on the full-duplex link
+  hipStream_t ws = nullptr, s_up = nullptr, s_down = nullptr;
   uint64_t bs = 0, bf = 0;
   Salts salts{};
   uint8_t cid_key[32]{};
@@ -285,8 +290,9 @@ struct glfsx_writer {
   std::vector<uint64_t> counts;
   uint64_t size = 0;
   PinBuf h_one;  // ctext of single posts (index nodes, the tail block)
-  WSlot slot[2];
+  WSlot slot[kSlots];
   int cur = 0;               // slot being filled
+  uint64_t seq = 0;
   uint64_t batch_blocks = 1;
   uint64_t full = 0;         // complete blocks staged in slot[cur]
   uint64_t partial = 0;      // bytes of the block being filled
@@ -317,9 +323,9 @@ int pin_grow(PinBuf &b, size_t need, size_t keep) {
 // Host copy into pinned staging; large copies are split over threads (the
 // Writer's memcpy into w.buf, blob.go:121-126, is its host-side cost).
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
-  constexpr size_t kMin = 8u << 20;
+  constexpr size_t kMin = 4u << 20;
   unsigned hw = std::thread::hardware_concurrency();
-  unsigned t = unsigned(std::min<size_t>(std::min(8u, hw ? hw : 1u), n / kMin));
+  unsigned t = unsigned(std::min<size_t>(std::min(16u, hw ? hw : 1u), n / kMin));
   if (t <= 1) {
     memcpy(dst, src, n);
     return;
@@ -408,12 +414,13 @@ int complete(glfsx_writer *w, WSlot &sl) {
 }
 
 // Enqueue the current slot's complete blocks (H2D, DEK + ChaCha/CID kernels,
-// D2H of refs and ctext), finish the other slot's batch, and switch slots,
-// carrying the partially filled block over.
+// D2H of refs and ctext), finish the oldest batch still in flight if it
+// holds the next slot, and switch slots, carrying the partial block over.
 int submit(glfsx_writer *w) {
   if (w->full == 0) return 0;
   WSlot &sl = w->slot[w->cur];
-  WSlot &nx = w->slot[w->cur ^ 1];
+  const int next = (w->cur + 1) % kSlots;
+  WSlot &nx = w->slot[next];
   const uint64_t nbytes = w->full * w->bs;
   if (int e = sl.d_in.ensure(nbytes)) return e;
   if (int e = sl.d_ct.ensure(nbytes)) return e;
@@ -421,8 +428,14 @@ int submit(glfsx_writer *w) {
   if (w->post)
     if (int e = sl.h_ct.ensure(nbytes + 64)) return e;
   if (int e = sl.h_refs.ensure(w->full * 64)) return e;
-  if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-  HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->ws));
+  if (!sl.done) {
+    HIP_TRY(hipEventCreateWithFlags(&sl.up, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&sl.hashed, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  }
+  HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->s_up));
+  HIP_TRY(hipEventRecord(sl.up, w->s_up));
+  HIP_TRY(hipStreamWaitEvent(w->ws, sl.up, 0));
   PostJob j{};
   j.src = sl.d_in.u8();
   j.ctext = sl.d_ct.u8();
@@ -434,17 +447,23 @@ int submit(glfsx_writer *w) {
   words_from_key(j.salt, w->salts.raw);
   cid_words(j, cidk(w));
   HIP_TRY(launch_post(j, w->ws));
+  HIP_TRY(hipEventRecord(sl.hashed, w->ws));
+  HIP_TRY(hipStreamWaitEvent(w->s_down, sl.hashed, 0));
   HIP_TRY(hipMemcpyAsync(sl.h_refs.p, sl.d_refs.p, w->full * 64,
-                         hipMemcpyDeviceToHost, w->ws));
+                         hipMemcpyDeviceToHost, w->s_down));
   if (w->post)
-    HIP_TRY(hipMemcpyAsync(sl.h_ct.p, sl.d_ct.p, nbytes, hipMemcpyDeviceToHost, w->ws));
-  HIP_TRY(hipEventRecord(sl.done, w->ws));
+    HIP_TRY(hipMemcpyAsync(sl.h_ct.p, sl.d_ct.p, nbytes, hipMemcpyDeviceToHost,
+                           w->s_down));
+  HIP_TRY(hipEventRecord(sl.done, w->s_down));
   sl.nblk = w->full;
+  sl.seq = ++w->seq;
   sl.busy = true;
-  if (int e = complete(w, nx)) return e;  // the previous batch, in order
+  // `nx` is the oldest batch in flight (submitted kSlots-1 batches ago):
+  // completing it keeps Posts in order
+  if (int e = complete(w, nx)) return e;
   if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
   if (w->partial) memcpy(nx.h_in.u8(), sl.h_in.u8() + nbytes, w->partial);
-  w->cur ^= 1;
+  w->cur = next;
   w->full = 0;
   return 0;
 }
@@ -659,7 +678,9 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   w->indexes.emplace_back(bs, 0);  // blob.go:111
   w->counts.push_back(0);
   w->batch_blocks = std::max<uint64_t>(1, (64ull << 20) / bs);
-  if (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->s_up, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->s_down, hipStreamNonBlocking) != hipSuccess) {
     delete w;
     *err = fail(GLFSX_E_DEVICE, "hipStreamCreate failed");
     return nullptr;
@@ -696,8 +717,13 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   if (!w || !out) return fail(GLFSX_E_ARG, "null argument");
   if (w->sticky) return w->sticky;
   if (int e = submit(w)) return w->sticky = e;
-  for (int k = 0; k < 2; ++k)  // at most one batch is still in flight
-    if (int e = complete(w, w->slot[w->cur ^ 1 ^ k])) return w->sticky = e;
+  for (;;) {  // drain the batches still in flight, oldest first
+    WSlot *o = nullptr;
+    for (auto &sl : w->slot)
+      if (sl.busy && (!o || sl.seq < o->seq)) o = &sl;
+    if (!o) break;
+    if (int e = complete(w, *o)) return w->sticky = e;
+  }
   if (w->partial) {  // blob.go:136-140: the tail block, never padded
     uint8_t ref[64];
     if (int e = post_one(w, 0, w->salts.raw, w->slot[w->cur].h_in.u8(), w->partial, ref))
@@ -716,7 +742,8 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
 
 void glfsx_writer_free(glfsx_writer *w) {
   if (!w) return;
-  if (w->ws) (void)hipStreamSynchronize(w->ws);
+  for (hipStream_t st : {w->s_up, w->ws, w->s_down})
+    if (st) (void)hipStreamSynchronize(st);
   for (auto &sl : w->slot) {
     if (sl.h_in.p) (void)hipHostFree(sl.h_in.p);
     if (sl.h_ct.p) (void)hipHostFree(sl.h_ct.p);
@@ -724,10 +751,12 @@ void glfsx_writer_free(glfsx_writer *w) {
     if (sl.d_in.p) (void)hipFree(sl.d_in.p);
     if (sl.d_ct.p) (void)hipFree(sl.d_ct.p);
     if (sl.d_refs.p) (void)hipFree(sl.d_refs.p);
-    if (sl.done) (void)hipEventDestroy(sl.done);
+    for (hipEvent_t ev : {sl.up, sl.hashed, sl.done})
+      if (ev) (void)hipEventDestroy(ev);
   }
   if (w->h_one.p) (void)hipHostFree(w->h_one.p);
-  if (w->ws) (void)hipStreamDestroy(w->ws);
+  for (hipStream_t st : {w->s_up, w->ws, w->s_down})
+    if (st) (void)hipStreamDestroy(st);
   delete w;
 }
 
