@@ -434,3 +434,52 @@ def test_decrypt_batch_roundtrip(gpu, O, bs, size):
     assert torch.equal(pt[:size], t[:size])
     r0 = host(refs, 64)
     assert O.chacha20_xor(host(ct, min(bs, size)), r0[32:]) == host(t, min(bs, size))
+
+
+# ------------------------------------------------- writer pipeline, extremes
+def test_writer_pipeline_many_batches(gpu, O):
+    """bs 4 KiB (bf 64): a 64 MiB batch holds 16384 blocks, so ~3 batches go
+    through the three-slot pipeline while index nodes are posted mid-batch;
+    the full Post sequence must equal the reference writer's."""
+    from glfs_amd import bigblob
+    bs = 4096
+    size = 3 * (64 << 20) + 12345
+    data = O.fill_splitmix(size, 77)
+    want_root, _, _, want_posts = O.create(data, bs, salt=None, chunks=[size // 3, size])
+    store = bigblob.MemStore(bs)
+    w = bigblob.Machine(bs).new_writer(store)
+    w.write(data[:size // 3])
+    w.write(data[size // 3:])
+    root = w.finish()
+    w.close()
+    assert root.ref.marshal_binary() == want_root
+    assert len(store.log) == len(want_posts)
+    assert [r for _, r, _ in store.log] == [r for _, r, _, _ in want_posts]
+
+
+def test_huge_block_size_g64(gpu, O):
+    """16 MiB blocks use the G = 64 kernels (64 chunks per lane)."""
+    from glfs_amd import bigblob
+    bs = 16 << 20
+    data = O.fill_splitmix(bs + 777, 8)
+    refs, ct = _post_batch_host(bytes(32), data, bs)
+    for j in range(2):
+        r, c = O.post(bytes(32), data[j * bs:(j + 1) * bs])
+        assert refs[64 * j:64 * j + 64] == r
+    assert bigblob.derive_key(bytes(32), data[:bs]) == O.derive_key(bytes(32), data[:bs])
+
+
+def test_writer_keyed_cid_and_tiny_writes(gpu, O):
+    """A store whose CID is keyed (cid_key), fed one byte at a time."""
+    from glfs_amd import bigblob
+    key = bytes(range(7, 39))
+    data = O.fill_splitmix(3000, 9)
+    want_root, _, _, want_posts = O.create(data, 1024, salt=None, cid_key=key)
+    store = bigblob.MemStore(1024)
+    w = bigblob.Machine(1024).new_writer(store, None, cid_key=key)
+    for i in range(len(data)):
+        w.write(data[i:i + 1])
+    root = w.finish()
+    w.close()
+    assert root.ref.marshal_binary() == want_root
+    assert [r for _, r, _ in store.log] == [r for _, r, _, _ in want_posts]
