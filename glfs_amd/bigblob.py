@@ -181,6 +181,10 @@ class Machine:
         """blob.go:85-114."""
         return Writer(self, store, salt, cid_key)
 
+    def concat(self, store, block_size: int, salt: Optional[bytes], *roots: Root) -> Root:
+        """blob.go:333-345."""
+        return _concat(self, store, block_size, salt, roots)
+
     def create(self, store: WO, salt: Optional[bytes], r,
                cid_key: Optional[bytes] = None) -> Root:
         """blob.go:209-217."""
@@ -190,6 +194,20 @@ class Machine:
             return w.finish()
         finally:
             w.close()
+
+
+def _concat(machine: "Machine", store, block_size: int, salt, roots, cid_key=None) -> Root:
+    """blob.go:333-345 Concat: read every root (GPU decrypt of each blob via
+    the read side), stream the bytes through a new Writer.  Like the
+    reference, the `block_size` argument is ignored: the writer uses the
+    machine's block size (quirk recorded in SURVEY's appendix)."""
+    w = machine.new_writer(store, salt, cid_key)
+    try:
+        for r in roots:
+            w.write(read_all(store, r))
+        return w.finish()
+    finally:
+        w.close()
 
 
 class MemStore:

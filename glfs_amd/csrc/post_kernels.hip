@@ -21,9 +21,6 @@
 // Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
 #include "kernels.h"
 
-#ifndef GLFSX_NT_CTEXT
-#define GLFSX_NT_CTEXT 0
-#endif
 
 namespace glfsx {
 namespace {
@@ -272,20 +269,10 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] ^= x[i];
     if (out) {
-#if GLFSX_NT_CTEXT
-      // ctext is written once and never re-read by this path: nontemporal
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 *o = reinterpret_cast<u32x4 *>(out);
-      __builtin_nontemporal_store(u32x4{m[0], m[1], m[2], m[3]}, o + 0);
-      __builtin_nontemporal_store(u32x4{m[4], m[5], m[6], m[7]}, o + 1);
-      __builtin_nontemporal_store(u32x4{m[8], m[9], m[10], m[11]}, o + 2);
-      __builtin_nontemporal_store(u32x4{m[12], m[13], m[14], m[15]}, o + 3);
-#else
       out[0] = make_uint4(m[0], m[1], m[2], m[3]);
       out[1] = make_uint4(m[4], m[5], m[6], m[7]);
       out[2] = make_uint4(m[8], m[9], m[10], m[11]);
       out[3] = make_uint4(m[12], m[13], m[14], m[15]);
-#endif
     }
   }
   b3_compress(cv, m, chunk, 0u, 64u, fl);

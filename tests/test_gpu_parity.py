@@ -483,3 +483,19 @@ def test_writer_keyed_cid_and_tiny_writes(gpu, O):
     w.close()
     assert root.ref.marshal_binary() == want_root
     assert [r for _, r, _ in store.log] == [r for _, r, _, _ in want_posts]
+
+
+def test_concat_vs_oracle(gpu, O):
+    """blob.go:333-345 Concat: the roots' bytes, read back through the GPU
+    decrypt, re-written as one blob == the oracle's Create of the joined
+    bytes; block_size is ignored as in the reference."""
+    from glfs_amd import bigblob
+    bs = 1024
+    store = bigblob.MemStore(bs)
+    m = bigblob.Machine(bs)
+    parts = [O.fill_splitmix(n, 50 + n) for n in (0, 5000, 1024, 16 * 1024 + 3)]
+    roots = [m.create(store, None, p) for p in parts]
+    got = m.concat(store, 12345, None, *roots)
+    want = O.create(b"".join(parts), bs, salt=None)[0]
+    assert got.ref.marshal_binary() == want
+    assert got.size == sum(map(len, parts))
