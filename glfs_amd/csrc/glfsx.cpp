@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -273,7 +274,9 @@ struct WSlot {
   bool busy = false;
 };
 
-constexpr int kSlots = 3;  // fill / upload+hash / download can all overlap
+// Batch slots: one being filled, one uploading/hashing, one downloading.
+// GLFSX_SLOTS (2..4) and GLFSX_BATCH_MIB override the defaults (tuning).
+constexpr int kMaxSlots = 4;
 
 struct glfsx_writer {
   Ctx *c = nullptr;
@@ -290,7 +293,8 @@ struct glfsx_writer {
   std::vector<uint64_t> counts;
   uint64_t size = 0;
   PinBuf h_one;  // ctext of single posts (index nodes, the tail block)
-  WSlot slot[kSlots];
+  WSlot slot[kMaxSlots];
+  int nslots = 3;
   int cur = 0;               // slot being filled
   uint64_t seq = 0;
   uint64_t batch_blocks = 1;
@@ -419,7 +423,7 @@ int complete(glfsx_writer *w, WSlot &sl) {
 int submit(glfsx_writer *w) {
   if (w->full == 0) return 0;
   WSlot &sl = w->slot[w->cur];
-  const int next = (w->cur + 1) % kSlots;
+  const int next = (w->cur + 1) % w->nslots;
   WSlot &nx = w->slot[next];
   const uint64_t nbytes = w->full * w->bs;
   if (int e = sl.d_in.ensure(nbytes)) return e;
@@ -458,7 +462,7 @@ int submit(glfsx_writer *w) {
   sl.nblk = w->full;
   sl.seq = ++w->seq;
   sl.busy = true;
-  // `nx` is the oldest batch in flight (submitted kSlots-1 batches ago):
+  // `nx` is the oldest batch in flight (submitted nslots-1 batches ago):
   // completing it keeps Posts in order
   if (int e = complete(w, nx)) return e;
   if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
@@ -677,7 +681,10 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   w->post_ctx = post_ctx;
   w->indexes.emplace_back(bs, 0);  // blob.go:111
   w->counts.push_back(0);
-  w->batch_blocks = std::max<uint64_t>(1, (64ull << 20) / bs);
+  uint64_t batch_mib = 64;
+  if (const char *e = getenv("GLFSX_BATCH_MIB")) batch_mib = std::max(1ull, strtoull(e, nullptr, 10));
+  if (const char *e = getenv("GLFSX_SLOTS")) w->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
+  w->batch_blocks = std::max<uint64_t>(1, (batch_mib << 20) / bs);
   if (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&w->s_up, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&w->s_down, hipStreamNonBlocking) != hipSuccess) {
