@@ -272,7 +272,30 @@ struct WSlot {
   uint64_t nblk = 0;  // blocks in flight
   uint64_t seq = 0;   // submission order
   bool busy = false;
+  int dev = -1;       // device of d_* (pool key)
 };
+
+// Staging slots outlive writers: glfs.PostBlob opens a Writer per blob
+// (machine.go:64), and pinned/device allocation costs far more than hashing a
+// small blob.  Freed writers return their slots here (per thread, bounded).
+thread_local std::vector<WSlot> tls_slot_pool;
+struct StreamTriple {
+  int dev;
+  hipStream_t up, hash, down;
+};
+thread_local std::vector<StreamTriple> tls_stream_pool;
+
+void release_slot(WSlot &sl) {
+  if (sl.h_in.p) (void)hipHostFree(sl.h_in.p);
+  if (sl.h_ct.p) (void)hipHostFree(sl.h_ct.p);
+  if (sl.h_refs.p) (void)hipHostFree(sl.h_refs.p);
+  if (sl.d_in.p) (void)hipFree(sl.d_in.p);
+  if (sl.d_ct.p) (void)hipFree(sl.d_ct.p);
+  if (sl.d_refs.p) (void)hipFree(sl.d_refs.p);
+  for (hipEvent_t ev : {sl.up, sl.hashed, sl.done})
+    if (ev) (void)hipEventDestroy(ev);
+  sl = WSlot();
+}
 
 // Batch slots: one being filled, one uploading/hashing, one downloading.
 // GLFSX_SLOTS (2..4) and GLFSX_BATCH_MIB override the defaults (tuning).
@@ -685,9 +708,29 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   if (const char *e = getenv("GLFSX_BATCH_MIB")) batch_mib = std::max(1ull, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GLFSX_SLOTS")) w->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
   w->batch_blocks = std::max<uint64_t>(1, (batch_mib << 20) / bs);
-  if (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&w->s_up, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&w->s_down, hipStreamNonBlocking) != hipSuccess) {
+  for (int k = 0; k < w->nslots; ++k) {
+    for (size_t i = tls_slot_pool.size(); i-- > 0;) {
+      if (tls_slot_pool[i].dev == c->dev) {
+        w->slot[k] = tls_slot_pool[i];
+        tls_slot_pool.erase(tls_slot_pool.begin() + i);
+        break;
+      }
+    }
+    w->slot[k].dev = c->dev;
+  }
+  for (size_t i = tls_stream_pool.size(); i-- > 0;) {
+    if (tls_stream_pool[i].dev == c->dev) {
+      w->s_up = tls_stream_pool[i].up;
+      w->ws = tls_stream_pool[i].hash;
+      w->s_down = tls_stream_pool[i].down;
+      tls_stream_pool.erase(tls_stream_pool.begin() + i);
+      break;
+    }
+  }
+  if (!w->ws &&
+      (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess ||
+       hipStreamCreateWithFlags(&w->s_up, hipStreamNonBlocking) != hipSuccess ||
+       hipStreamCreateWithFlags(&w->s_down, hipStreamNonBlocking) != hipSuccess)) {
     delete w;
     *err = fail(GLFSX_E_DEVICE, "hipStreamCreate failed");
     return nullptr;
@@ -752,18 +795,20 @@ void glfsx_writer_free(glfsx_writer *w) {
   for (hipStream_t st : {w->s_up, w->ws, w->s_down})
     if (st) (void)hipStreamSynchronize(st);
   for (auto &sl : w->slot) {
-    if (sl.h_in.p) (void)hipHostFree(sl.h_in.p);
-    if (sl.h_ct.p) (void)hipHostFree(sl.h_ct.p);
-    if (sl.h_refs.p) (void)hipHostFree(sl.h_refs.p);
-    if (sl.d_in.p) (void)hipFree(sl.d_in.p);
-    if (sl.d_ct.p) (void)hipFree(sl.d_ct.p);
-    if (sl.d_refs.p) (void)hipFree(sl.d_refs.p);
-    for (hipEvent_t ev : {sl.up, sl.hashed, sl.done})
-      if (ev) (void)hipEventDestroy(ev);
+    sl.busy = false;
+    sl.nblk = 0;
+    if (sl.dev >= 0 && tls_slot_pool.size() < 2 * kMaxSlots)
+      tls_slot_pool.push_back(sl);  // buffers are reused by the next writer
+    else
+      release_slot(sl);
   }
   if (w->h_one.p) (void)hipHostFree(w->h_one.p);
-  for (hipStream_t st : {w->s_up, w->ws, w->s_down})
-    if (st) (void)hipStreamDestroy(st);
+  if (w->ws && tls_stream_pool.size() < 4) {
+    tls_stream_pool.push_back({w->c->dev, w->s_up, w->ws, w->s_down});
+  } else {
+    for (hipStream_t st : {w->s_up, w->ws, w->s_down})
+      if (st) (void)hipStreamDestroy(st);
+  }
   delete w;
 }
 
