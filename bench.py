@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 # VALU lane-instructions per plaintext byte, measured with rocprofv3
 # SQ_INSTS_VALU x 64 / bytes (profiles/r1/summary.json).
-INSTR_PER_BYTE = {"dek": 12.11, "cid": 27.12}
+INSTR_PER_BYTE = {"dek": 11.66, "cid": 26.41}
 
 
 def parse():
