@@ -21,6 +21,10 @@
 // Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
 #include "kernels.h"
 
+#ifndef GLFSX_LDS_CTEXT
+#define GLFSX_LDS_CTEXT 1
+#endif
+
 
 namespace glfsx {
 namespace {
@@ -254,13 +258,34 @@ __device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
 
 // One full 64-B block of the fast path: (ChaCha20 keystream XOR, ctext
 // store,) BLAKE3 compression.
-template <bool CHACHA>
+// LDS staging of ctext (GLFSX_LDS_CTEXT): each wave owns 64 lines x 128 B;
+// lane c puts 16-B piece p of its current 128-B line at byte
+// c*128 + ((p ^ ((c>>1)&7)) << 4) (conflict-free ds_write_b128 in 8-lane
+// groups and ds_read_b128 in its 16-lane groups), then the wave stores 8 full
+// lines per buffer_store_dwordx4 instead of 64 sixteenths of lines.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+__device__ __forceinline__ uint32_t lds_offset(const void *p) {
+  return uint32_t(reinterpret_cast<uintptr_t>(
+      (const __attribute__((address_space(3))) void *)p));
+}
+
+// opaque to the optimiser: keeps per-piece addresses from being hoisted
+// into 8-16 loop-invariant VGPRs (1 v_xor each instead)
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+template <bool CHACHA, bool STAGE = false>
 __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
                                            const uint4 &w1, const uint4 &w2,
                                            const uint4 &w3, uint32_t chunk,
                                            uint32_t b, uint32_t fl,
                                            const uint32_t (&dek)[8],
-                                           uint4 *out) {
+                                           uint4 *out, uint32_t wa = 0,
+                                           uint32_t half = 0) {
   uint32_t m[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
                     w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
   if constexpr (CHACHA) {
@@ -268,7 +293,13 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
     chacha_block(x, dek, (chunk << 4) + b);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] ^= x[i];
-    if (out) {
+    if (STAGE) {  // LDS staging: wa = this lane's swizzled line address
+      wa = opaque(wa);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<lds_u32x4 *>(wa ^ ((4u * half + q) << 4)) =
+            u32x4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
+    } else if (out) {
       out[0] = make_uint4(m[0], m[1], m[2], m[3]);
       out[1] = make_uint4(m[4], m[5], m[6], m[7]);
       out[2] = make_uint4(m[8], m[9], m[10], m[11]);
@@ -284,11 +315,11 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
 // next even block's before the odd one, so HBM latency is covered and no
 // buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
 // the chaining-value reset are per-chunk (scalar), not per-block selects.
-template <int G, bool CHACHA>
+template <int G, bool CHACHA, bool STAGE = false>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
-    const uint32_t (&dek)[8]) {
+    const uint32_t (&dek)[8], uint32_t sbase = 0, uint32_t clen = 0) {
   constexpr int D = ilog2(G);
   constexpr uint32_t NB = 16u * G;
   uint32_t stk[D > 0 ? D : 1][8];
@@ -297,6 +328,15 @@ __device__ __forceinline__ void lane_subtree_full(
   uint4 *cq = cmsg ? reinterpret_cast<uint4 *>(cmsg + (uint64_t(first) << 10))
                    : nullptr;
   uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  // staging (sbase != 0, whole wave on this path, cmsg = message base):
+  const uint32_t l = threadIdx.x & 63u, r = l >> 3, pc = l & 7u;
+  const uint32_t wa = STAGE ? sbase + (l << 7) + (((l >> 1) & 7u) << 4) : 0u;
+  const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
+  // store voffset of (line r of this wave's 8-line group 0, piece pc)
+  const uint32_t vo = ((threadIdx.x - l + r) * uint32_t(G) << 10) + (pc << 4);
+  // message-uniform descriptor (cmsg, clen are workgroup-uniform)
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      cmsg, 0, STAGE ? clen : 0u, 0x00020000);
   for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
     const uint32_t chunk = first + jj;
 #pragma unroll
@@ -305,9 +345,10 @@ __device__ __forceinline__ void lane_subtree_full(
       const uint32_t blk = jj * 16 + 2 * pp;
       const uint4 *nb = q + 4 * (blk + 1);
       uint4 b0 = nb[0], b1 = nb[1], b2 = nb[2], b3 = nb[3];
-      full_block<CHACHA>(cv, a0, a1, a2, a3, chunk, 2 * pp,
+      constexpr bool stg = CHACHA && STAGE;
+      full_block<CHACHA, stg>(cv, a0, a1, a2, a3, chunk, 2 * pp,
                          base | (pp == 0 ? kChunkStart : 0u), dek,
-                         cq ? cq + 4 * blk : nullptr);
+                         cq && !stg ? cq + 4 * blk : nullptr, wa, 0);
       if (blk + 2 < NB) {
         const uint4 *na = q + 4 * (blk + 2);
         a0 = na[0];
@@ -317,8 +358,21 @@ __device__ __forceinline__ void lane_subtree_full(
       }
       uint32_t fl = base;
       if (pp == 7) fl |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
-      full_block<CHACHA>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
-                         cq ? cq + 4 * (blk + 1) : nullptr);
+      full_block<CHACHA, stg>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
+                         cq && !stg ? cq + 4 * (blk + 1) : nullptr, wa, 1);
+      if (stg) {
+        // lane l stores piece pc of line 8k + r: each store instruction
+        // writes 8 whole 128-B lines.  Line 8k+r's slot for pc is
+        // rb ^ ((k&1) << 6) + k*1024 (the swizzle's bit 2 is k's parity).
+        const uint32_t r0 = opaque(rb), r1 = r0 ^ 64u, v0 = vo + blk * 64u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const u32x4 v = *reinterpret_cast<const lds_u32x4 *>(
+              ((k & 1) ? r1 : r0) + 1024u * k);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v0,
+              (8u * k * uint32_t(G)) << 10, 0);
+        }
+      }
     }
     lane_merge<D>(cv, stk, depth, jj, jj + 1 == uint32_t(G), whole, key, base);
   }
@@ -390,7 +444,11 @@ __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t (&w)[8
 
 template <int G, bool CHACHA, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
-  __shared__ uint32_t lds[256 * 8];
+  // one LDS array: [0, 8 KiB) CV tree; CHACHA && GLFSX_LDS_CTEXT: + 4 waves x
+  // 8 KiB ctext staging
+  constexpr int kStageU4 = (CHACHA && GLFSX_LDS_CTEXT) ? 4 * 512 : 0;
+  __shared__ uint4 lds_u4[512 + kStageU4];
+  uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
   const uint64_t j = blockIdx.x;
   const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
   const uint8_t *msg = a.src + j * a.stride;
@@ -427,9 +485,18 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   const uint32_t first = t * G;
   const uint32_t n_my = first < C ? min(uint32_t(G), C - first) : 0u;
   uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ALIGNED && n_my == uint32_t(G) &&
-      len >= (uint64_t(first) + G) << 10) {
-    lane_subtree_full<G, CHACHA>(cv, msg, cmsg, first, whole, key, a.base, dek);
+  const bool fast = ALIGNED && n_my == uint32_t(G) &&
+                    len >= (uint64_t(first) + G) << 10;
+  // staged stores write other lanes' lines: only when the whole wave is fast
+  const bool wave_fast = __ballot(fast) == ~0ull;
+  if (fast) {
+    if (kStageU4 && wave_fast && cmsg)  // wave-uniform
+      lane_subtree_full<G, CHACHA, kStageU4 != 0>(
+          cv, msg, cmsg, first, whole, key, a.base, dek,
+          lds_offset(lds_u4 + 512 + (t >> 6) * 512), uint32_t(len));
+    else
+      lane_subtree_full<G, CHACHA>(cv, msg, cmsg, first, whole, key, a.base,
+                                   dek);
   } else if (n_my) {
     lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
                                      key, a.base, dek);

@@ -415,6 +415,15 @@ int main(int argc, char **argv) {
     for (uint64_t b = 0; b < n; ++b)
       if (memcmp(h1.data() + 64 * b, h2.data() + 64 * b, 64)) ++bad;
     printf("cid v1 vs v2: %zu / %llu refs differ\n", bad, (unsigned long long)n);
+    // ctext fingerprint (compare across GLFSX_LDS_CTEXT builds)
+    const size_t cn = size_t(1) << 28;
+    std::vector<uint64_t> hc(cn / 8);
+    uint64_t fp = 1469598103934665603ull;
+    for (uint64_t off = 0; off < total; off += total / 4) {
+      CK(hipMemcpy(hc.data(), d_ct + off, cn, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < hc.size(); ++i) fp = (fp ^ hc[i]) * 1099511628211ull;
+    }
+    printf("ctext fingerprint: %016llx\n", (unsigned long long)fp);
   }
   const uint32_t iters = 4096;
   const uint32_t grid = 256 * 8 * 4;  // 8 waves / SIMD worth of 256-thr WGs
