@@ -24,6 +24,9 @@
 #ifndef GLFSX_LDS_CTEXT
 #define GLFSX_LDS_CTEXT 1
 #endif
+#ifndef GLFSX_LDS_LOADS
+#define GLFSX_LDS_LOADS 1
+#endif
 
 
 namespace glfsx {
@@ -327,29 +330,76 @@ __device__ __forceinline__ void lane_subtree_full(
   const uint4 *q = reinterpret_cast<const uint4 *>(msg + (uint64_t(first) << 10));
   uint4 *cq = cmsg ? reinterpret_cast<uint4 *>(cmsg + (uint64_t(first) << 10))
                    : nullptr;
-  uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-  // staging (sbase != 0, whole wave on this path, cmsg = message base):
+  // LDS staging (STAGE: sbase = this wave's 8 KiB, the whole wave is on
+  // this path).  CHACHA: ctext staged for full-line stores.  !CHACHA (DEK
+  // pass): plaintext loaded by buffer_load ... lds, 8 full lines per
+  // instruction, one pair of blocks ahead, into the same swizzled image.
+  constexpr bool gl = !CHACHA && STAGE;
+  uint4 a0, a1, a2, a3;
+  if constexpr (!gl) {
+    a0 = q[0];
+    a1 = q[1];
+    a2 = q[2];
+    a3 = q[3];
+  }
   const uint32_t l = threadIdx.x & 63u, r = l >> 3, pc = l & 7u;
   const uint32_t wa = STAGE ? sbase + (l << 7) + (((l >> 1) & 7u) << 4) : 0u;
+  const uint32_t wst = CHACHA ? wa : 0u;  // full_block's staging target
   const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
   // store voffset of (line r of this wave's 8-line group 0, piece pc)
   const uint32_t vo = ((threadIdx.x - l + r) * uint32_t(G) << 10) + (pc << 4);
-  // message-uniform descriptor (cmsg, clen are workgroup-uniform)
+  // message-uniform descriptor (cmsg / msg, clen are workgroup-uniform)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      cmsg, 0, STAGE ? clen : 0u, 0x00020000);
+      gl ? const_cast<uint8_t *>(msg) : cmsg, 0, STAGE ? clen : 0u, 0x00020000);
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
+  // gl: source of (line 8k+r, image slot pc) = piece pc ^ swizzle(8k+r)
+  const uint32_t lo0 = vo - (pc << 4) + ((pc ^ (r >> 1)) << 4);
+  auto issue = [&](uint32_t s) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
+          16, (k & 1) ? (lo0 ^ 64u) : lo0, ((8u * k * uint32_t(G)) << 10) + 128u * s,
+          0, 0);
+  };
+  if constexpr (gl) issue(0);
   for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
     const uint32_t chunk = first + jj;
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = key[i];
     for (uint32_t pp = 0; pp < 8; ++pp) {
       const uint32_t blk = jj * 16 + 2 * pp;
-      const uint4 *nb = q + 4 * (blk + 1);
-      uint4 b0 = nb[0], b1 = nb[1], b2 = nb[2], b3 = nb[3];
+      uint4 b0, b1, b2, b3;
+      if constexpr (gl) {
+        // this pair's lines have landed; take them, then refill the image
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 v[8];
+        const uint32_t w = opaque(wa);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          v[i] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(i) << 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blk + 2 < NB) issue(blk / 2 + 1);
+        a0 = make_uint4(v[0].x, v[0].y, v[0].z, v[0].w);
+        a1 = make_uint4(v[1].x, v[1].y, v[1].z, v[1].w);
+        a2 = make_uint4(v[2].x, v[2].y, v[2].z, v[2].w);
+        a3 = make_uint4(v[3].x, v[3].y, v[3].z, v[3].w);
+        b0 = make_uint4(v[4].x, v[4].y, v[4].z, v[4].w);
+        b1 = make_uint4(v[5].x, v[5].y, v[5].z, v[5].w);
+        b2 = make_uint4(v[6].x, v[6].y, v[6].z, v[6].w);
+        b3 = make_uint4(v[7].x, v[7].y, v[7].z, v[7].w);
+      } else {
+        const uint4 *nb = q + 4 * (blk + 1);
+        b0 = nb[0];
+        b1 = nb[1];
+        b2 = nb[2];
+        b3 = nb[3];
+      }
       constexpr bool stg = CHACHA && STAGE;
       full_block<CHACHA, stg>(cv, a0, a1, a2, a3, chunk, 2 * pp,
                          base | (pp == 0 ? kChunkStart : 0u), dek,
-                         cq && !stg ? cq + 4 * blk : nullptr, wa, 0);
-      if (blk + 2 < NB) {
+                         cq && !stg ? cq + 4 * blk : nullptr, wst, 0);
+      if (!gl && blk + 2 < NB) {
         const uint4 *na = q + 4 * (blk + 2);
         a0 = na[0];
         a1 = na[1];
@@ -359,7 +409,7 @@ __device__ __forceinline__ void lane_subtree_full(
       uint32_t fl = base;
       if (pp == 7) fl |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
       full_block<CHACHA, stg>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
-                         cq && !stg ? cq + 4 * (blk + 1) : nullptr, wa, 1);
+                         cq && !stg ? cq + 4 * (blk + 1) : nullptr, wst, 1);
       if (stg) {
         // lane l stores piece pc of line 8k + r: each store instruction
         // writes 8 whole 128-B lines.  Line 8k+r's slot for pc is
@@ -444,9 +494,10 @@ __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t (&w)[8
 
 template <int G, bool CHACHA, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
-  // one LDS array: [0, 8 KiB) CV tree; CHACHA && GLFSX_LDS_CTEXT: + 4 waves x
-  // 8 KiB ctext staging
-  constexpr int kStageU4 = (CHACHA && GLFSX_LDS_CTEXT) ? 4 * 512 : 0;
+  // one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext
+  // in the CHACHA pass, plaintext in the DEK pass): 40 KiB, 4 WGs per CU
+  constexpr int kStageU4 =
+      (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
   __shared__ uint4 lds_u4[512 + kStageU4];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
   const uint64_t j = blockIdx.x;
@@ -490,7 +541,7 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   // staged stores write other lanes' lines: only when the whole wave is fast
   const bool wave_fast = __ballot(fast) == ~0ull;
   if (fast) {
-    if (kStageU4 && wave_fast && cmsg)  // wave-uniform
+    if (kStageU4 && wave_fast && (cmsg || !CHACHA))  // wave-uniform
       lane_subtree_full<G, CHACHA, kStageU4 != 0>(
           cv, msg, cmsg, first, whole, key, a.base, dek,
           lds_offset(lds_u4 + 512 + (t >> 6) * 512), uint32_t(len));
