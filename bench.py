@@ -257,10 +257,34 @@ def cpu_baseline(args):
     t = time.perf_counter()
     L.oracle_post_batch(refs, ct, bytes(32), buf, n, args.block_size, None, 1)
     dt = time.perf_counter() - t
+    del buf, ct
+    # all host cores this job may use, independent block
+    # ranges (the box exports its CPU share as OMP_NUM_THREADS)
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(),
+                       os.cpu_count()))
+    n2 = 4 * n
+    buf = ctypes.create_string_buffer(n2)
+    ct = ctypes.create_string_buffer(n2)
+    L.oracle_fill_splitmix(buf, 0, n2, args.seed)
+    refs = ctypes.create_string_buffer(64 * (n2 // args.block_size))
+    t = time.perf_counter()
+    L.oracle_post_batch(refs, ct, bytes(32), buf, n2, args.block_size, None, cores)
+    dt2 = time.perf_counter() - t
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f
+                          if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(n / GIB / dt, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{args.cpu_sample_mib} MiB = {n // args.block_size} x "
                       f"{args.block_size // 1024} KiB blocks, oracle_post_batch, 1 thread, "
-                      f"{dt:.1f} s"}
+                      f"{dt:.1f} s",
+            "all_cores": {"value": round(n2 / GIB / dt2, 4), "cores": cores,
+                          "sample": f"{4 * args.cpu_sample_mib} MiB, {cores} threads over "
+                                    f"independent block ranges, {dt2:.1f} s"},
+            "cpu_model": model}
 
 
 def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=5):

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import io
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import BinaryIO, Optional, Protocol, Union
 
@@ -21,6 +22,7 @@ CID_SIZE = 32          # blobcache.CIDSize [ext]
 REF_SIZE = CID_SIZE + DEK_SIZE  # ref.go:52
 MAX_REF_SIZE = REF_SIZE         # index.go:6
 KIND_DATA, KIND_INDEX = 0, 1
+KIND_COPY = 2  # a blob copied by Sync (its kind is not known to the copier)
 
 
 @dataclass(frozen=True)
@@ -175,6 +177,108 @@ class Machine:
             raise Panic(N.GLFSX_E_ARG, str(block_size))
         self.block_size = block_size
         self.cache_size = cache_size
+        # machine.go:36 getF LRU, keyed by Ref.Key() (= BLAKE3(CID||DEK) in
+        # the reference; the 64-B ref itself identifies the same entry)
+        self._cache: "OrderedDict[bytes, bytes]" = OrderedDict()
+
+    # ------------------------------------------------------------ read side
+    def get_f(self, store, ref: Ref) -> bytes:
+        """ref.go:113-126 getF: fetch the ctext by CID, decrypt with the DEK
+        (ChaCha20 on the GPU), cache the plaintext."""
+        key = ref.marshal_binary()
+        hit = self._cache.get(key)
+        if hit is not None:
+            self._cache.move_to_end(key)
+            return hit
+        data = crypto_xor(ref.dek, store.get(ref.cid))
+        if self.cache_size > 0:
+            self._cache[key] = data
+            if len(self._cache) > self.cache_size:
+                self._cache.popitem(last=False)
+        return data
+
+    def get_piece(self, store, root: Ref, bf: int, level: int, block_index: int) -> Ref:
+        """blob.go:53-69 getPiece: walk index nodes down to the block's ref.
+        Index nodes must be exactly bf*64 bytes (newIndexUsing)."""
+        while level > 0:
+            data = self.get_f(store, root)
+            if len(data) != bf * MAX_REF_SIZE:
+                raise ValueError("data is not correct size for index")
+            span = bf ** (level - 1)
+            i = block_index // span
+            root = Ref.from_bytes(data[i * MAX_REF_SIZE:(i + 1) * MAX_REF_SIZE])
+            block_index %= span
+            level -= 1
+        return root
+
+    def read_at(self, store, x: Root, offset: int, n: int) -> tuple:
+        """blob.go:31-51 ReadAt: at most ONE block per call (quirk kept).
+        Returns (data, eof) where eof mirrors the io.EOF the reference
+        returns when the read ends exactly at Size."""
+        level = depth(x.size, x.block_size)
+        bf = branching_factor(x.block_size)
+        block_index, rel = divmod(offset, x.block_size)
+        ref = self.get_piece(store, x.ref, bf, level, block_index)
+        data = self.get_f(store, ref)
+        if rel > len(data):  # Go slices data[relOffset:] and panics
+            raise Panic(N.GLFSX_E_ARG, "slice bounds out of range")
+        out = data[rel:rel + n]
+        return out, offset + len(out) == x.size
+
+    def new_reader(self, store, root: Root) -> "Reader":
+        """io.go:23-30."""
+        return Reader(self, store, root)
+
+    def traverse(self, store, root: Root, enter, exit) -> None:
+        """traverse.go:18-52: pre-order Enter(cid) -> bool (False skips the
+        subtree), post-order Exit(level, ref).  Children stop at the first
+        all-zero CID."""
+        if root.block_size == 0:
+            raise ValueError("block size cannot be zero")
+        self._traverse(store, root.block_size, depth(root.size, root.block_size),
+                       root.ref, enter, exit)
+
+    def _traverse(self, store, bs, level, x: Ref, enter, exit) -> None:
+        if not enter(x.cid):
+            return
+        if level > 0:
+            data = self.get_f(store, x)
+            if len(data) != bs:
+                raise ValueError("data is not correct size for index")
+            for i in range(bs // MAX_REF_SIZE):
+                r2 = Ref.from_bytes(data[i * MAX_REF_SIZE:(i + 1) * MAX_REF_SIZE])
+                if r2.cid == bytes(CID_SIZE):
+                    break
+                self._traverse(store, bs, level - 1, r2, enter, exit)
+        exit(level, x)
+
+    def sync(self, dst, src, x: Root, fn=None) -> None:
+        """blob.go:270-315 Sync: nothing to do if dst has the root CID;
+        otherwise call fn(reader), then copy every reachable blob (children
+        before their index node)."""
+        if exists_unit(dst, x.ref.cid):
+            return
+        if fn is not None:
+            fn(self.new_reader(src, x))
+        self._sync(dst, src, x.block_size, x.ref, depth(x.size, x.block_size))
+
+    def _sync(self, dst, src, bs, ref: Ref, level: int) -> None:
+        if level > 0:
+            data = self.get_f(src, ref)
+            if len(data) != bs:
+                raise ValueError("data is not correct size for index")
+            for i in range(bs // MAX_REF_SIZE):
+                r2 = Ref.from_bytes(data[i * MAX_REF_SIZE:(i + 1) * MAX_REF_SIZE])
+                if r2.cid == bytes(CID_SIZE):
+                    break
+                self._sync(dst, src, bs, r2, level - 1)
+        copy_blob(dst, src, ref)
+
+    def populate(self, store, root: Root, dst) -> None:
+        """blob.go:317-331 Populate: add every reachable CID that dst lacks
+        (Enter skips subtrees dst already has; Exit adds)."""
+        self.traverse(store, root, lambda cid: not exists_unit(dst, cid),
+                      lambda level, ref: dst.add(ref.cid))
 
     def new_writer(self, store: WO, salt: Optional[bytes] = None,
                    cid_key: Optional[bytes] = None) -> Writer:
@@ -208,6 +312,69 @@ def _concat(machine: "Machine", store, block_size: int, salt, roots, cid_key=Non
         return w.finish()
     finally:
         w.close()
+
+
+class Reader:
+    """io.go:15-54 Reader: Read / ReadAt / Seek over a Root (each call reads
+    from at most one block, as the reference's ReadAt does)."""
+    SEEK_SET, SEEK_CUR, SEEK_END = 0, 1, 2
+
+    def __init__(self, machine: Machine, store, root: Root):
+        self.o, self.store, self.root, self.offset = machine, store, root, 0
+
+    def read_at(self, n: int, at: int) -> tuple:
+        return self.o.read_at(self.store, self.root, at, n)
+
+    def read(self, n: int = -1) -> bytes:
+        """Python io semantics on top of ReadAt: returns b"" at EOF; n < 0
+        reads to the end (block by block)."""
+        if self.offset >= self.root.size:
+            return b""
+        if n < 0:
+            parts = []
+            while self.offset < self.root.size:
+                parts.append(self.read(self.root.size - self.offset))
+            return b"".join(parts)
+        data, _ = self.o.read_at(self.store, self.root, self.offset, n)
+        self.offset += len(data)
+        return data
+
+    def seek(self, offset: int, whence: int = 0) -> int:
+        if whence == self.SEEK_SET:
+            self.offset = offset
+        elif whence == self.SEEK_CUR:
+            self.offset += offset
+        elif whence == self.SEEK_END:
+            self.offset = self.root.size + offset
+        else:
+            raise Panic(N.GLFSX_E_ARG, "invalid whence")
+        return self.offset
+
+
+def exists_unit(store, cid: bytes) -> bool:
+    """machine.go:86-92 ExistsUnit."""
+    return bool(store.exists(cid))
+
+
+def copy_blob(dst, src, ref: Ref) -> None:
+    """blob.go:306-315 copyBlob: Get the ctext from src, Post it to dst.
+    The destination is a pre-hashed store (its Post takes the CID with the
+    bytes), so the copy keeps the CID the source holds."""
+    ct = src.get(ref.cid)
+    dst.post(ct, ref.cid + bytes(DEK_SIZE), KIND_COPY)
+
+
+class CIDSet:
+    """A minimal AddExister (machine.go:81-84): Exists + Add over CIDs."""
+
+    def __init__(self):
+        self.cids: set = set()
+
+    def exists(self, cid: bytes) -> bool:
+        return cid in self.cids
+
+    def add(self, cid: bytes) -> None:
+        self.cids.add(cid)
 
 
 class MemStore:

@@ -34,6 +34,14 @@ class Ref:
         return d
 
 
+class ErrRefType(TypeError):
+    """errors.go:20-26."""
+
+    def __init__(self, have: str, want: str):
+        super().__init__(f"wrong type HAVE: {have} WANT: {want}")
+        self.have, self.want = have, want
+
+
 def with_salt(salt: bytes):
     """machine.go:15-19 WithSalt -- dead: NewMachine never applies options."""
     def opt(m: "Machine") -> None:
@@ -118,6 +126,49 @@ class Machine:
     def new_blob_writer(self, store) -> TypedWriter:
         """blob.go:37-39."""
         return self.new_typed_writer(store, TYPE_BLOB)
+
+    # ------------------------------------------------------------ read side
+    def get_typed(self, store, ty: str, x: Ref) -> bigblob.Reader:
+        """glfs.go:59-66 GetTyped (ty "" accepts any type)."""
+        if ty and x.type != ty:
+            raise ErrRefType(x.type, ty)
+        return self.bbag.new_reader(store, x.root)
+
+    def get_blob(self, store, x: Ref) -> bigblob.Reader:
+        """blob.go:20-22, 33-35."""
+        return self.get_typed(store, TYPE_BLOB, x)
+
+    def get_blob_bytes(self, store, x: Ref, max_size: int) -> bytes:
+        """blob.go:25-31 (readAtMost: more than max_size bytes is an error)."""
+        r = self.get_blob(store, x)
+        if x.root.size > max_size:
+            raise ValueError(f"blob exceeds max size {max_size}")
+        return r.read()
+
+    # ---------------------------------------------------------------- trees
+    def new_tree_writer(self, store, **kw):
+        """tree.go:290-298."""
+        from .tree import TreeWriter
+        return TreeWriter(self, store, **kw)
+
+    def post_tree(self, store, ents, **kw) -> Ref:
+        """tree.go:195-238."""
+        from .tree import post_tree
+        return post_tree(self, store, ents, **kw)
+
+    def post_tree_slice(self, store, ents, **kw) -> Ref:
+        """tree.go:240-247."""
+        return self.post_tree(store, list(ents), **kw)
+
+    def post_tree_map(self, store, m: dict, **kw) -> Ref:
+        """tree.go:249-260."""
+        from .tree import post_tree_map
+        return post_tree_map(self, store, m, **kw)
+
+    def get_tree_slice(self, store, ref: Ref, max_ents: int = 10 ** 6, **kw) -> list:
+        """tree.go:137-143."""
+        from .tree import get_tree_slice
+        return get_tree_slice(store, ref, max_ents, **kw)
 
 
 _default: Optional[Machine] = None

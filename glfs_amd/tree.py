@@ -1,0 +1,305 @@
+"""Trees: the glfs directory object over the GPU write path.
+
+Reference: tree.go (blobcache/glfs, Go).  A tree is a typed blob (type
+"tree", typeSalt = DeriveKey(0^32, "tree")) whose bytes are JSON lines, one
+TreeEntry per line, sorted by name (tree.go:284-320 TreeWriter, 195-238
+PostTree).  The bytes go through the same bigblob Writer (GPU DEK + ChaCha20 +
+CID) as every blob.
+
+The line format is Go's ``json.Encoder.Encode(TreeEntry)`` (go 1.25, go.mod:3):
+``{"name":N,"mode":M,"ref":{"type":T,"cid":C,"dek":"<hex>","size":S,"blockSize":B}}\\n``
+with field order from the struct tags (tree.go:74-78, glfs.go:35-38,
+bigblob/blob.go:17-21, bigblob/ref.go:54-57) and Go's string escaping (HTML
+characters as \\u003c/\\u003e/\\u0026, U+2028/2029 escaped, \\b \\f \\n \\r \\t,
+other control bytes as \\u00XX, invalid UTF-8 as U+FFFD).
+
+PARITY UNPINNED at one field: ``cid`` is blobcache.CID's JSON form, which
+lives in the blobcache module (go.mod:16) and is absent here.  The encoder is
+a parameter (``cid_json``); the default writes the lower-case hex string.
+Everything else in the line is fixed by the reference.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass
+from typing import Callable, Iterable, Optional
+
+from . import bigblob
+from . import glfs
+from .bigblob import Root
+
+MODE_DIR = 1 << 31          # os.ModeDir
+MODE_FILE = 0o644           # tree.go:262-267 getFileMode
+MODE_TREE = 0o755 | MODE_DIR
+
+
+class TreeError(ValueError):
+    """The errors tree.go returns with fmt.Errorf / errors.New."""
+
+
+@dataclass(frozen=True)
+class TreeEntry:
+    """tree.go:74-78 TreeEntry{Name, FileMode, Ref}."""
+    name: str
+    file_mode: int
+    ref: glfs.Ref
+
+    def validate(self) -> None:
+        """tree.go:80-89."""
+        if clean_path(self.name) != self.name:
+            raise TreeError(f"name ({self.name}) is not properly cleaned")
+        if self.name == "":
+            raise TreeError("TreeEntry name cannot be empty")
+
+
+def get_file_mode(ref: glfs.Ref) -> int:
+    """tree.go:262-267."""
+    return MODE_TREE if ref.type == glfs.TYPE_TREE else MODE_FILE
+
+
+def _go_path_clean(p: str) -> str:
+    """Go path.Clean (lexical): collapse //, drop ., resolve .. where it can."""
+    if p == "":
+        return "."
+    rooted = p.startswith("/")
+    out: list[str] = []
+    for part in p.split("/"):
+        if part in ("", "."):
+            continue
+        if part == "..":
+            if out and out[-1] != "..":
+                out.pop()
+            elif not rooted:
+                out.append("..")
+            continue
+        out.append(part)
+    s = "/".join(out)
+    if rooted:
+        return "/" + s
+    return s or "."
+
+
+def clean_path(x: str) -> str:
+    """tree.go:269-277 CleanPath."""
+    x = _go_path_clean(x).strip("/")
+    return "" if x == "." else x
+
+
+def is_valid_name(x: str) -> bool:
+    """tree.go:279-282."""
+    return x != "" and "/" not in x
+
+
+def _name_key(name: str) -> bytes:
+    # strings.Compare is byte-wise on the UTF-8 encoding
+    return name.encode("utf-8", "surrogatepass")
+
+
+def sort_tree_entries(ents: list) -> None:
+    """tree.go:32-34 (slices.SortFunc by name)."""
+    ents.sort(key=lambda e: _name_key(e.name))
+
+
+def validate_tree_entries(ents: list) -> None:
+    """tree.go:36-50."""
+    keys = [_name_key(e.name) for e in ents]
+    if keys != sorted(keys):
+        raise TreeError("tree entries are not sorted")
+    for a, b in zip(ents, ents[1:]):
+        if a.name == b.name:
+            raise TreeError(f"duplicate tree entry {a} {b}")
+    for e in ents:
+        e.validate()
+
+
+def lookup(ents: list, name: str) -> Optional[TreeEntry]:
+    """tree.go:22-30 (binary search over sorted entries)."""
+    lo, hi, k = 0, len(ents), _name_key(name)
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if _name_key(ents[mid].name) < k:
+            lo = mid + 1
+        else:
+            hi = mid
+    if lo < len(ents) and ents[lo].name == name:
+        return ents[lo]
+    return None
+
+
+# ------------------------------------------------------------------- JSON
+_ESC = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t",
+        "\b": "\\b", "\f": "\\f", "<": "\\u003c", ">": "\\u003e", "&": "\\u0026",
+        "\u2028": "\\u2028", "\u2029": "\\u2029"}
+
+
+def go_json_string(s: str) -> str:
+    """encoding/json string encoding with HTML escaping (Encoder default)."""
+    out = ['"']
+    for ch in s:
+        e = _ESC.get(ch)
+        if e is not None:
+            out.append(e)
+        elif ch < " ":
+            out.append("\\u%04x" % ord(ch))
+        elif 0xD800 <= ord(ch) <= 0xDFFF:  # a lone surrogate = invalid UTF-8
+            out.append("\ufffd")
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def cid_json_hex(cid: bytes) -> str:
+    """Default CID JSON form (parity unpinned, see module docstring)."""
+    return '"' + cid.hex() + '"'
+
+
+def ref_json(ref: glfs.Ref, cid_json: Callable[[bytes], str] = cid_json_hex) -> str:
+    """glfs.Ref as encoding/json writes it: Type, then the promoted fields of
+    the embedded bigblob.Root (cid, dek, size, blockSize)."""
+    r = ref.root
+    return ('{"type":' + go_json_string(ref.type) + ',"cid":' + cid_json(r.ref.cid)
+            + ',"dek":"' + r.ref.dek.hex() + '","size":' + str(r.size)
+            + ',"blockSize":' + str(r.block_size) + "}")
+
+
+def entry_json_line(te: TreeEntry, cid_json: Callable[[bytes], str] = cid_json_hex) -> bytes:
+    """json.Encoder.Encode(te): one line, trailing newline."""
+    s = ('{"name":' + go_json_string(te.name) + ',"mode":' + str(te.file_mode)
+         + ',"ref":' + ref_json(te.ref, cid_json) + "}\n")
+    return s.encode("utf-8")
+
+
+def _cid_from_json(v) -> bytes:
+    if isinstance(v, str):
+        return bytes.fromhex(v)
+    raise TreeError(f"cannot decode cid {v!r}")
+
+
+def entry_from_json(obj: dict, cid_from_json=_cid_from_json) -> TreeEntry:
+    r = obj["ref"]
+    root = Root(bigblob.Ref(cid_from_json(r["cid"]), bytes.fromhex(r["dek"])),
+                int(r["size"]), int(r["blockSize"]))
+    return TreeEntry(obj["name"], int(obj["mode"]), glfs.Ref(r["type"], root))
+
+
+# ------------------------------------------------------------------ writer
+class TreeWriter:
+    """tree.go:284-320.  Put checks order and referential integrity, then
+    json-encodes the entry into a TypedWriter("tree").  Lines are handed to
+    the bigblob Writer in runs that end exactly where the reference's Writer
+    would post a chunk, so a store error surfaces at the same Put."""
+
+    def __init__(self, machine: "glfs.Machine", store,
+                 cid_json: Callable[[bytes], str] = cid_json_hex):
+        self.dst = store
+        self.tw = machine.new_typed_writer(store, glfs.TYPE_TREE)
+        self.cid_json = cid_json
+        self.last_name = ""
+        self._pending: list = []
+        self._pending_len = 0
+        self._written = 0
+        self._bs = machine.block_size
+
+    def put(self, te: TreeEntry) -> None:
+        """tree.go:295-312."""
+        if _name_key(te.name) <= _name_key(self.last_name):
+            raise TreeError(f"cannot write tree entries out of order "
+                            f"{te.name!r} <= {self.last_name!r}")
+        if not exists_unit(self.dst, te.ref.root.ref.cid):
+            raise TreeError(f"adding tree ent {te} would violate referential integrity")
+        line = entry_json_line(te, self.cid_json)
+        self._pending.append(line)
+        self._pending_len += len(line)
+        # the reference Writer posts when its buffer reaches a block: flush
+        # everything pending on the Put that crosses a block boundary
+        if (self._written + self._pending_len) // self._bs > self._written // self._bs:
+            self._flush()
+        self.last_name = te.name
+
+    def _flush(self) -> None:
+        if self._pending:
+            data = b"".join(self._pending)
+            self._pending, self._pending_len = [], 0
+            self.tw.write(data)
+            self._written += len(data)
+
+    def finish(self) -> glfs.Ref:
+        """tree.go:315-317."""
+        try:
+            self._flush()
+            return self.tw.finish()
+        finally:
+            self.tw.bw.close()
+
+
+def exists_unit(store, cid: bytes) -> bool:
+    """bigblob.ExistsUnit [ext store]: the store's Exists for one CID."""
+    return bool(store.exists(cid))
+
+
+def post_tree(machine: "glfs.Machine", store, ents: Iterable[TreeEntry],
+              cid_json: Callable[[bytes], str] = cid_json_hex) -> glfs.Ref:
+    """tree.go:195-238 PostTree: entries may carry paths; subdirectories are
+    posted first (recursively), then this level's sorted entries."""
+    root_ents: list = []
+    subents: dict = {}
+    for ent in ents:
+        p = clean_path(ent.name)
+        if p == "":
+            return ent.ref
+        parts = p.split("/", 1)
+        if len(parts) == 1:
+            root_ents.append(TreeEntry(parts[0], ent.file_mode, ent.ref))
+        else:
+            subents.setdefault(parts[0], []).append(
+                TreeEntry(parts[1], ent.file_mode, ent.ref))
+    for k, ents2 in subents.items():
+        ref = post_tree(machine, store, ents2, cid_json)
+        root_ents.append(TreeEntry(k, get_file_mode(ref), ref))
+    sort_tree_entries(root_ents)
+    tw = TreeWriter(machine, store, cid_json)
+    try:
+        for ent in root_ents:
+            tw.put(ent)
+    except BaseException:
+        tw.tw.bw.close()
+        raise
+    return tw.finish()
+
+
+def post_tree_map(machine: "glfs.Machine", store, m: dict,
+                  cid_json: Callable[[bytes], str] = cid_json_hex) -> glfs.Ref:
+    """tree.go:249-260 PostTreeMap."""
+    return post_tree(machine, store,
+                     [TreeEntry(k, get_file_mode(v), v) for k, v in m.items()], cid_json)
+
+
+# ------------------------------------------------------------------ reader
+def read_tree_bytes(data: bytes, cid_from_json=_cid_from_json) -> list:
+    """TreeReader.Next over the decoded bytes (tree.go:340-372): a stream of
+    JSON values, each a TreeEntry, strictly increasing names, each valid."""
+    dec = json.JSONDecoder()
+    s = data.decode("utf-8", "replace")
+    i, n, out, last = 0, len(s), [], ""
+    while True:
+        while i < n and s[i] in " \t\r\n":
+            i += 1
+        if i >= n:
+            return out
+        obj, i = dec.raw_decode(s, i)
+        te = entry_from_json(obj, cid_from_json)
+        if _name_key(te.name) <= _name_key(last):
+            raise TreeError(f"tree entries are out of order: {te.name} <= {last}")
+        te.validate()
+        last = te.name
+        out.append(te)
+
+
+def get_tree_slice(store, ref: glfs.Ref, max_ents: int = 10 ** 6,
+                   cid_from_json=_cid_from_json) -> list:
+    """tree.go:137-143 GetTreeSlice (the read side decrypts on the GPU)."""
+    if ref.type != glfs.TYPE_TREE:
+        raise TreeError(f"wrong ref type: have {ref.type} want {glfs.TYPE_TREE}")
+    ents = read_tree_bytes(bigblob.read_all(store, ref.root), cid_from_json)
+    return ents[:max_ents]
