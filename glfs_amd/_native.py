@@ -59,6 +59,7 @@ SIGNATURES = {
     "glfsx_device_count": (_INT, []),
     "glfsx_set_device": (_INT, [_INT]),
     "glfsx_version": (_CP, []),
+    "glfsx_set_split_target": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),
     "glfsx_post_batch": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch_device": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP, _VP]),
@@ -136,3 +137,10 @@ def device_count() -> int:
 
 def set_device(dev: int) -> None:
     check(lib.glfsx_set_device(dev))
+
+
+def set_split_target(wgs: int) -> int:
+    """Tuning knob (include/glfsx.h): launches of fewer than `wgs` workgroups
+    spread each block over several workgroups.  0 disables.  Returns the
+    previous value."""
+    return lib.glfsx_set_split_target(wgs)

@@ -75,6 +75,11 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
 hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
                        hipStream_t s);
 
+// Split mode (post_kernels.hip launch_pass): a launch of fewer than `wgs`
+// workgroups spreads each message over up to 64 workgroups.  0 disables it.
+// Returns the previous value.
+uint32_t set_split_target(uint32_t wgs);
+
 void words_from_key(uint32_t w[8], const uint8_t key[32]);
 void blake3_iv_words(uint32_t w[8]);
 

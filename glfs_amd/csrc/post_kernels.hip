@@ -21,6 +21,9 @@
 // Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
 #include "kernels.h"
 
+#include <atomic>
+#include <cstdlib>
+
 #ifndef GLFSX_LDS_CTEXT
 #define GLFSX_LDS_CTEXT 1
 #endif
@@ -217,6 +220,12 @@ struct KArgs {
   uint32_t key[8];
   uint32_t base;     // kKeyed or 0
   uint32_t out_off;  // byte offset of the 32-byte result inside the ref slot
+  // split mode (few messages): 2^split_log2 workgroups per message, each over
+  // 256*G consecutive chunks; their subtree CVs go to scratch (8 words per
+  // workgroup) and k_merge finishes the tree.  split_log2 == 0: one
+  // workgroup per message, no scratch.
+  uint32_t split_log2;
+  uint32_t *scratch;
 };
 
 // Merge step after the last block of local chunk jj: pop/parent/push on the
@@ -322,7 +331,8 @@ template <int G, bool CHACHA, bool STAGE = false>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
-    const uint32_t (&dek)[8], uint32_t sbase = 0, uint32_t clen = 0) {
+    const uint32_t (&dek)[8], uint32_t sbase = 0, uint32_t clen = 0,
+    uint32_t cbase = 0) {
   constexpr int D = ilog2(G);
   constexpr uint32_t NB = 16u * G;
   uint32_t stk[D > 0 ? D : 1][8];
@@ -364,7 +374,9 @@ __device__ __forceinline__ void lane_subtree_full(
   };
   if constexpr (gl) issue(0);
   for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
-    const uint32_t chunk = first + jj;
+    // absolute chunk index (BLAKE3 chunk counter, ChaCha block counter / 16);
+    // msg points at chunk cbase of the message
+    const uint32_t chunk = cbase + first + jj;
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = key[i];
     for (uint32_t pp = 0; pp < 8; ++pp) {
@@ -436,13 +448,14 @@ template <int G, bool CHACHA, bool ALIGNED>
 __device__ __forceinline__ void lane_subtree(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint64_t len,
     uint32_t first, uint32_t n_my, bool whole, const uint32_t (&key)[8],
-    uint32_t base, const uint32_t (&dek)[8]) {
+    uint32_t base, const uint32_t (&dek)[8], uint32_t cbase = 0) {
   constexpr int D = ilog2(G);
   uint32_t stk[D > 0 ? D : 1][8];
   uint32_t depth = 0;
   for (uint32_t jj = 0; jj < n_my; ++jj) {
-    const uint32_t chunk = first + jj;
-    const uint64_t coff = uint64_t(chunk) << 10;
+    const uint32_t lchunk = first + jj;           // within msg[0, len)
+    const uint32_t chunk = cbase + lchunk;        // counter: absolute index
+    const uint64_t coff = uint64_t(lchunk) << 10;
     const uint64_t rem = len - coff;
     const uint32_t clen = rem < 1024 ? uint32_t(rem) : 1024u;
     const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
@@ -492,6 +505,41 @@ __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t (&w)[8
   }
 }
 
+// Pairwise merge of the k subtree CVs in lds[0 .. 8k) (all but the last are
+// perfect subtrees of one power-of-two size, so this is BLAKE3's left-complete
+// tree); the last parent gets ROOT when `root`.  Every thread of the block
+// calls it; on return thread 0 holds the result in p (p = its own value on
+// entry when k == 1).
+__device__ __forceinline__ void tree_reduce(uint32_t *lds, uint32_t k,
+                                            uint32_t t, const uint32_t (&key)[8],
+                                            uint32_t base, bool root,
+                                            uint32_t (&p)[8]) {
+  while (k > 1) {
+    const uint32_t half = k >> 1, odd = k & 1u;
+    if (t < half) {
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        m[i] = lds[(2 * t) * 8 + i];
+        m[8 + i] = lds[(2 * t + 1) * 8 + i];
+        p[i] = key[i];
+      }
+      b3_compress(p, m, 0u, 0u, 64u,
+                  base | kParent | ((root && k == 2) ? kRoot : 0u));
+    } else if (odd && t == half) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) p[i] = lds[(k - 1) * 8 + i];
+    }
+    __syncthreads();
+    if (t < half + odd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[t * 8 + i] = p[i];
+    }
+    __syncthreads();
+    k = half + odd;
+  }
+}
+
 template <int G, bool CHACHA, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   // one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext
@@ -500,10 +548,18 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
       (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
   __shared__ uint4 lds_u4[512 + kStageU4];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
-  const uint64_t j = blockIdx.x;
-  const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
-  const uint8_t *msg = a.src + j * a.stride;
-  uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + j * a.stride : nullptr;
+  // message j, sub-range sidx (split mode) = chunks [sidx*256G, +256G)
+  const uint64_t j = blockIdx.x >> a.split_log2;
+  const uint32_t sidx = blockIdx.x & ((1u << a.split_log2) - 1u);
+  const uint64_t len_full = (j + 1 == a.n) ? a.last_len : a.msg_len;
+  constexpr uint64_t kSpan = uint64_t(256 * G) << 10;  // bytes per workgroup
+  const uint64_t c0b = uint64_t(sidx) * kSpan;
+  if (sidx != 0 && c0b >= len_full) return;  // empty sub-range (uniform)
+  const uint64_t len = min(len_full - c0b, kSpan);
+  const bool split = len_full > kSpan;  // the message spans > 1 workgroup
+  const uint32_t cbase = sidx * uint32_t(256 * G);
+  const uint8_t *msg = a.src + j * a.stride + c0b;
+  uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + j * a.stride + c0b : nullptr;
   uint8_t *ref = a.refs + (j / a.ref_bf) * a.ref_stride + (j % a.ref_bf) * 64;
   const uint32_t t = threadIdx.x;
 
@@ -532,7 +588,7 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   }
 
   const uint32_t C = len ? uint32_t((len + 1023) >> 10) : 1u;
-  const bool whole = C <= uint32_t(G);
+  const bool whole = !split && C <= uint32_t(G);
   const uint32_t first = t * G;
   const uint32_t n_my = first < C ? min(uint32_t(G), C - first) : 0u;
   uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -544,13 +600,13 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
     if (kStageU4 && wave_fast && (cmsg || !CHACHA))  // wave-uniform
       lane_subtree_full<G, CHACHA, kStageU4 != 0>(
           cv, msg, cmsg, first, whole, key, a.base, dek,
-          lds_offset(lds_u4 + 512 + (t >> 6) * 512), uint32_t(len));
+          lds_offset(lds_u4 + 512 + (t >> 6) * 512), uint32_t(len), cbase);
     else
       lane_subtree_full<G, CHACHA>(cv, msg, cmsg, first, whole, key, a.base,
-                                   dek);
+                                   dek, 0u, 0u, cbase);
   } else if (n_my) {
     lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
-                                     key, a.base, dek);
+                                     key, a.base, dek, cbase);
   }
   if (whole) {  // uniform: depends on len only; lane 0 holds the root output
     if (t == 0) store_digest(ref + a.out_off, cv);
@@ -562,32 +618,45 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
     for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
   }
   __syncthreads();
-  uint32_t k = active;
-  while (k > 1) {
-    const uint32_t half = k >> 1, odd = k & 1u;
-    uint32_t p[8];
-    if (t < half) {
-      uint32_t m[16];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        m[i] = lds[(2 * t) * 8 + i];
-        m[8 + i] = lds[(2 * t + 1) * 8 + i];
-        p[i] = key[i];
-      }
-      b3_compress(p, m, 0u, 0u, 64u, a.base | kParent | (k == 2 ? kRoot : 0u));
-    } else if (odd && t == half) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) p[i] = lds[(k - 1) * 8 + i];
+  tree_reduce(lds, active, t, key, a.base, !split, cv);
+  if (t == 0) {
+    if (split) {  // this workgroup's subtree CV, finished by k_merge
+      uint4 *q = reinterpret_cast<uint4 *>(a.scratch + uint64_t(blockIdx.x) * 8);
+      q[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+      q[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+    } else {
+      store_digest(ref + a.out_off, cv);
     }
-    __syncthreads();
-    if (t < half + odd) {
+  }
+}
+
+// Split mode, second phase: one 64-lane workgroup per message merges the
+// subtree CVs of its W = ceil(len / span) workgroups (W <= 64) and writes the
+// root output.  Messages that fit one workgroup were finished by k_pass.
+__global__ __launch_bounds__(64) void k_merge(KArgs a, uint64_t span) {
+  __shared__ uint32_t lds[64 * 8];
+  const uint64_t j = blockIdx.x;
+  const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
+  if (len <= span) return;
+  const uint32_t W = uint32_t((len + span - 1) / span);
+  const uint32_t t = threadIdx.x;
+  uint32_t key[8], p[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) lds[t * 8 + i] = p[i];
-    }
-    __syncthreads();
-    k = half + odd;
-    // the last level (k == 2 -> 1) is computed by lane 0: the ROOT output
-    if (k == 1 && t == 0) store_digest(ref + a.out_off, p);
+  for (int i = 0; i < 8; ++i) key[i] = a.key[i];
+  if (t < W) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(
+        a.scratch + ((j << a.split_log2) + t) * 8);
+    const uint4 x = q[0], y = q[1];
+    p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
+    p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[t * 8 + i] = p[i];
+  }
+  __syncthreads();
+  tree_reduce(lds, W, t, key, a.base, true, p);
+  if (t == 0) {
+    uint8_t *ref = a.refs + (j / a.ref_bf) * a.ref_stride + (j % a.ref_bf) * 64;
+    store_digest(ref + a.out_off, p);
   }
 }
 
@@ -720,30 +789,83 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, uint64_t offset,
 
 template <int G, bool CHACHA>
 hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
-  const dim3 grid(uint32_t(a.n)), block(256);
+  const dim3 grid(uint32_t(a.n << a.split_log2)), block(256);
   if (aligned)
     hipLaunchKernelGGL((k_pass<G, CHACHA, true>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL((k_pass<G, CHACHA, false>), grid, block, 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || a.split_log2 == 0) return e;
+  hipLaunchKernelGGL(k_merge, dim3(uint32_t(a.n)), dim3(64), 0, s, a,
+                     uint64_t(256 * G) << 10);
   return hipGetLastError();
 }
 
+// Split-mode target: workgroups per launch below which a message is spread
+// over more workgroups (fewer chunks per lane).  0 disables split mode.
+// GLFSX_SPLIT_WG overrides the default (tuning, A/B runs).
+uint32_t split_target_default() {
+  const char *e = getenv("GLFSX_SPLIT_WG");
+  return e ? uint32_t(strtoul(e, nullptr, 10)) : 2048u;
+}
+std::atomic<uint32_t> g_split_target{split_target_default()};
+constexpr uint32_t kMaxSplitLog2 = 6;  // k_merge merges <= 64 subtrees
+
+// Stream-ordered scratch for split mode (a few bytes per workgroup).  The
+// device pool keeps freed blocks (release threshold = max), so steady-state
+// allocations are pool hits, not hipMalloc calls.
+hipError_t scratch_alloc(uint32_t **p, size_t bytes, hipStream_t s) {
+  static std::atomic<uint64_t> pools_done{0};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 64 && !(pools_done.load() & (1ull << dev))) {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t thr = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    pools_done.fetch_or(1ull << dev);
+  }
+  return hipMallocAsync(reinterpret_cast<void **>(p), bytes, s);
+}
+
 template <bool CHACHA>
-hipError_t launch_pass(const KArgs &a, uint64_t maxlen, bool aligned,
+hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
                        hipStream_t s) {
   const uint64_t C = maxlen ? (maxlen + 1023) >> 10 : 1;
   int g = 1;
   while (256ull * g < C) g *= 2;
-  switch (g) {
-    case 1: return launch_g<1, CHACHA>(a, aligned, s);
-    case 2: return launch_g<2, CHACHA>(a, aligned, s);
-    case 4: return launch_g<4, CHACHA>(a, aligned, s);
-    case 8: return launch_g<8, CHACHA>(a, aligned, s);
-    case 16: return launch_g<16, CHACHA>(a, aligned, s);
-    case 32: return launch_g<32, CHACHA>(a, aligned, s);
-    case 64: return launch_g<64, CHACHA>(a, aligned, s);
-    default: return hipErrorInvalidValue;
+  // few messages: halve the chunks per lane and double the workgroups per
+  // message until the launch fills the chip (256 CUs x 8 workgroups)
+  uint32_t sl = 0;
+  const uint64_t target = g_split_target.load(std::memory_order_relaxed);
+  while (g > 1 && sl < kMaxSplitLog2 && (a.n << sl) < target) {
+    g /= 2;
+    ++sl;
   }
+  a.split_log2 = sl;
+  a.scratch = nullptr;
+  if (sl) {
+    hipError_t e = scratch_alloc(&a.scratch, size_t(a.n << sl) * 32, s);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e;
+  switch (g) {
+    case 1: e = launch_g<1, CHACHA>(a, aligned, s); break;
+    case 2: e = launch_g<2, CHACHA>(a, aligned, s); break;
+    case 4: e = launch_g<4, CHACHA>(a, aligned, s); break;
+    case 8: e = launch_g<8, CHACHA>(a, aligned, s); break;
+    case 16: e = launch_g<16, CHACHA>(a, aligned, s); break;
+    case 32: e = launch_g<32, CHACHA>(a, aligned, s); break;
+    case 64: e = launch_g<64, CHACHA>(a, aligned, s); break;
+    default: e = hipErrorInvalidValue;
+  }
+  if (a.scratch) {
+    hipError_t f = hipFreeAsync(a.scratch, s);
+    if (e == hipSuccess) e = f;
+  }
+  return e;
 }
 
 template <bool CHACHA>
@@ -789,6 +911,8 @@ void words_from_key(uint32_t w[8], const uint8_t key[32]) {
     w[i] = uint32_t(key[4 * i]) | (uint32_t(key[4 * i + 1]) << 8) |
            (uint32_t(key[4 * i + 2]) << 16) | (uint32_t(key[4 * i + 3]) << 24);
 }
+
+uint32_t set_split_target(uint32_t wgs) { return g_split_target.exchange(wgs); }
 
 void blake3_iv_words(uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) w[i] = kIV[i];

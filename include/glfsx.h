@@ -83,6 +83,12 @@ const char *glfsx_last_error(void);
 int glfsx_device_count(void);
 int glfsx_set_device(int dev);      /* for the calling thread */
 const char *glfsx_version(void);
+/* Tuning (no reference counterpart): a hashing launch of fewer than `wgs`
+ * 256-lane workgroups spreads each block over up to 64 workgroups plus a
+ * merge launch (index nodes, 1-2 GiB blobs, Writer batches).  0 disables
+ * it; the default is 2048.  Results are identical either way.  Returns the
+ * previous value; process-wide. */
+uint32_t glfsx_set_split_target(uint32_t wgs);
 
 /* --- primitives -------------------------------------------------------- */
 /* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input, first out_len

@@ -104,6 +104,62 @@ def test_post_batch_vs_oracle(gpu, O, bs):
             assert ct[j * bs:j * bs + len(blk)] == c, (bs, total, j)
 
 
+@pytest.fixture
+def split_target():
+    """Restores the split-mode target (include/glfsx.h) after a test."""
+    from glfs_amd import _native as N
+    old = N.set_split_target(2048)
+    N.set_split_target(old)
+    yield N.set_split_target
+    N.set_split_target(old)
+
+
+@pytest.mark.parametrize("bs,total", [(1 << 20, (3 << 20) + 5), (1 << 20, 9 << 20),
+                                      (2 << 20, (5 << 20) + 999), (5 << 20, 11 << 20),
+                                      (300_000, 2_000_003), (65536, 65536 * 3 + 1),
+                                      (1024, 5000), (16 << 20, (16 << 20) + 1)])
+def test_split_modes_vs_oracle(gpu, O, split_target, bs, total):
+    """Split mode (several workgroups per block + merge launch) vs one
+    workgroup per block vs the oracle: refs and ctext bit-exact.  Targets:
+    0 = never split, 2048 = default, 2**31 = split every block maximally."""
+    rng = random.Random(bs ^ total)
+    salt = bytes(rng.randrange(256) for _ in range(32))
+    data = O.fill_splitmix(total, total + 3)
+    outs = []
+    for target in (0, 2048, 1 << 31):
+        split_target(target)
+        outs.append(_post_batch_host(salt, data, bs))
+        outs.append(_post_batch_host(salt, data, bs, cid_key=bytes(range(32))))
+    assert outs[0] == outs[2] == outs[4]
+    assert outs[1] == outs[3] == outs[5]
+    refs, ct = outs[0]
+    for j in range(0, (total + bs - 1) // bs):
+        blk = data[j * bs:(j + 1) * bs]
+        r, c = O.post(salt, blk)
+        assert refs[64 * j:64 * j + 64] == r, (bs, total, j)
+        assert ct[j * bs:j * bs + len(blk)] == c, (bs, total, j)
+    j = rng.randrange((total + bs - 1) // bs)
+    r, _ = O.post(salt, data[j * bs:(j + 1) * bs], cid_key=bytes(range(32)))
+    assert outs[1][0][64 * j:64 * j + 64] == r
+
+
+def test_split_modes_create_device(gpu, O, split_target):
+    """Index levels in split mode: a 3-level tree at 4 KiB blocks and a
+    17-block blob at 1 MiB, roots equal across targets and to the oracle."""
+    torch = _torch()
+    for bs, size in [(4096, 4096 * 64 * 2 + 7), (1 << 20, (17 << 20) + 5)]:
+        t = dev_bytes(torch, size, seed=size)
+        roots = set()
+        for target in (0, 2048, 1 << 31):
+            split_target(target)
+            roots.add(_create_device(torch, bs, t, size))
+        assert len(roots) == 1
+        want, _, _, want_posts = O.create(O.fill_splitmix(size, size), bs, salt=None,
+                                          closed_form=True)
+        root, posts = roots.pop()
+        assert root == want and posts == len(want_posts)
+
+
 def test_post_batch_keyed_cid(gpu, O):
     key = bytes(range(100, 132))
     data = O.fill_splitmix(5 * 4096 + 17, 11)
