@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libglfsx.so")
+# GLFSX_LIB: an alternative build of the same library (A/B tuning runs only)
+LIB_PATH = os.environ.get("GLFSX_LIB") or os.path.join(_HERE, "libglfsx.so")
 
 GLFSX_OK = 0
 GLFSX_E_BLOCKSIZE_GT_MAX = -1

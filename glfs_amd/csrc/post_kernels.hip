@@ -30,6 +30,12 @@
 #ifndef GLFSX_LDS_LOADS
 #define GLFSX_LDS_LOADS 1
 #endif
+// CID pass: plaintext also arrives by buffer_load ... lds, into the ctext
+// staging image (in place: the lane takes its pair out, writes the ctext pair
+// back into the same slots, the wave stores full lines, then refills).
+#ifndef GLFSX_CID_LDS_LOADS
+#define GLFSX_CID_LDS_LOADS 1
+#endif
 
 
 namespace glfsx {
@@ -344,7 +350,9 @@ __device__ __forceinline__ void lane_subtree_full(
   // this path).  CHACHA: ctext staged for full-line stores.  !CHACHA (DEK
   // pass): plaintext loaded by buffer_load ... lds, 8 full lines per
   // instruction, one pair of blocks ahead, into the same swizzled image.
-  constexpr bool gl = !CHACHA && STAGE;
+  // CHACHA && gl: the image is shared by the plaintext pair (landing) and
+  // the ctext pair (leaving), so the next pair is issued after the stores
+  constexpr bool gl = STAGE && (!CHACHA || GLFSX_CID_LDS_LOADS);
   uint4 a0, a1, a2, a3;
   if constexpr (!gl) {
     a0 = q[0];
@@ -360,7 +368,9 @@ __device__ __forceinline__ void lane_subtree_full(
   const uint32_t vo = ((threadIdx.x - l + r) * uint32_t(G) << 10) + (pc << 4);
   // message-uniform descriptor (cmsg / msg, clen are workgroup-uniform)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      gl ? const_cast<uint8_t *>(msg) : cmsg, 0, STAGE ? clen : 0u, 0x00020000);
+      CHACHA ? cmsg : const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_ld = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
   const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
   // gl: source of (line 8k+r, image slot pc) = piece pc ^ swizzle(8k+r)
   const uint32_t lo0 = vo - (pc << 4) + ((pc ^ (r >> 1)) << 4);
@@ -368,7 +378,7 @@ __device__ __forceinline__ void lane_subtree_full(
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsrc, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
+          rsrc_ld, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
           16, (k & 1) ? (lo0 ^ 64u) : lo0, ((8u * k * uint32_t(G)) << 10) + 128u * s,
           0, 0);
   };
@@ -391,7 +401,7 @@ __device__ __forceinline__ void lane_subtree_full(
         for (int i = 0; i < 8; ++i)
           v[i] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(i) << 4));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (blk + 2 < NB) issue(blk / 2 + 1);
+        if (!CHACHA && blk + 2 < NB) issue(blk / 2 + 1);
         a0 = make_uint4(v[0].x, v[0].y, v[0].z, v[0].w);
         a1 = make_uint4(v[1].x, v[1].y, v[1].z, v[1].w);
         a2 = make_uint4(v[2].x, v[2].y, v[2].z, v[2].w);
@@ -433,6 +443,10 @@ __device__ __forceinline__ void lane_subtree_full(
               ((k & 1) ? r1 : r0) + 1024u * k);
           __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v0,
               (8u * k * uint32_t(G)) << 10, 0);
+        }
+        if (gl && blk + 2 < NB) {  // the image is free again: next pair
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          issue(blk / 2 + 1);
         }
       }
     }
