@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 # VALU lane-instructions per plaintext byte, measured with rocprofv3
 # SQ_INSTS_VALU x 64 / bytes (profiles/r1/summary.json).
-INSTR_PER_BYTE = {"dek": 11.66, "cid": 26.41}
+INSTR_PER_BYTE = {"dek": 11.60, "cid": 26.53}
 
 
 def parse():
@@ -240,7 +240,9 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get(dom, {}).get("hbm_bytes_per_launch")
+            t = json.load(open(tf)).get(dom, {})
+            # profiled at the 64 GiB launch; traffic is linear in blocks
+            traffic = int(t["hbm_bytes_per_launch"] * alg[dom] / t["algorithmic_bytes"])
         except Exception:
             traffic = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
