@@ -364,9 +364,11 @@ __device__ __forceinline__ void lane_subtree_full(
   const uint32_t wa = STAGE ? sbase + (l << 7) + (((l >> 1) & 7u) << 4) : 0u;
   const uint32_t wst = CHACHA ? wa : 0u;  // full_block's staging target
   const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
-  // store voffset of (line r of this wave's 8-line group 0, piece pc)
-  const uint32_t vo = ((threadIdx.x - l + r) * uint32_t(G) << 10) + (pc << 4);
-  // message-uniform descriptor (cmsg / msg, clen are workgroup-uniform)
+  // store voffset of (line r of this wave's 8-line group 0, piece pc); lane
+  // l's data starts at chunk `first` of msg and lane 0's at first - l*G
+  // (k_pass: first = t*G; k_small: msg = the wave's base, first = l*G)
+  const uint32_t vo = ((first + (r - l) * uint32_t(G)) << 10) + (pc << 4);
+  // wave-uniform descriptors (msg / cmsg, clen uniform over the wave)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       CHACHA ? cmsg : const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsrc_ld = __builtin_amdgcn_make_buffer_rsrc(
@@ -694,6 +696,8 @@ struct SArgs {
 
 template <int G, bool CHACHA>
 __global__ __launch_bounds__(256) void k_small(SArgs a) {
+  // 4 waves x 8 KiB staging image (same layout as k_pass's)
+  __shared__ uint4 lds_u4[4 * 512];
   const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
   if (i >= a.n) return;  // no barriers in this kernel
   const uint64_t off = a.offs[i], len = a.lens[i];
@@ -715,12 +719,26 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
   const bool aligned = ((reinterpret_cast<uintptr_t>(msg) |
                          reinterpret_cast<uintptr_t>(cmsg)) & 15) == 0;
   uint32_t cv[8];
-  if (aligned && len == uint64_t(G) << 10)
+  // a full wave of back-to-back blobs of exactly G KiB (config 4: 4 KiB
+  // blobs packed densely) has k_pass's lane layout: stage through LDS for
+  // full-line loads (and ctext stores)
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t o0 = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(off >> 32))) << 32) |
+                      __builtin_amdgcn_readfirstlane(uint32_t(off));
+  const bool dense = aligned && len == uint64_t(G) << 10 &&
+                     off == o0 + (uint64_t(l) * G << 10) && (!CHACHA || cmsg);
+  if (__ballot(dense) == ~0ull) {  // wave-uniform
+    lane_subtree_full<G, CHACHA, true>(
+        cv, a.src + o0, cmsg ? a.ctext + o0 : nullptr, l * G, true, key, a.base,
+        dek, lds_offset(lds_u4 + (threadIdx.x >> 6) * 512), 64u * G << 10,
+        0u - l * G);
+  } else if (aligned && len == uint64_t(G) << 10) {
     lane_subtree_full<G, CHACHA>(cv, msg, cmsg, 0u, true, key, a.base, dek);
-  else if (aligned)
+  } else if (aligned) {
     lane_subtree<G, CHACHA, true>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
-  else
+  } else {
     lane_subtree<G, CHACHA, false>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
+  }
   store_digest(ref + a.out_off, cv);
 }
 
@@ -730,7 +748,9 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
 __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
   const uint64_t per = a.msg_len >> 6;  // keystream blocks per bigblob block
   const uint64_t total_kb = (a.n - 1) * per + ((a.last_len + 63) >> 6);
-  for (uint64_t kb = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; kb < total_kb;
+  // a.stride: first keystream block (the part before it went through
+  // k_decrypt_lines)
+  for (uint64_t kb = a.stride + blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; kb < total_kb;
        kb += uint64_t(gridDim.x) * blockDim.x) {
     const uint64_t j = kb / per;
     const uint32_t ctr = uint32_t(kb - j * per);
@@ -751,6 +771,71 @@ __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
     for (int i = 0; i < 16; ++i) m[i] ^= x[i];
     if (al) store_block<true>(a.ctext + off, m, avail);
     else store_block<false>(a.ctext + off, m, avail);
+  }
+}
+
+// Read side, bulk: one wave per 8 KiB of ctext (lane l = 128-B line l = two
+// keystream blocks), bs % 8192 == 0 so the wave's DEK is uniform (SGPRs; the
+// key-only quarter-rounds of round 1 are hoisted by the compiler).  Lines
+// arrive by buffer_load ... lds (8 full lines per instruction) into the
+// swizzled image of k_pass, each lane takes its line, XORs the keystream,
+// writes it back in place, and the wave stores 8 full lines per instruction.
+// Covers whole 8 KiB units [0, a.n_units); k_decrypt does the rest.
+__global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units) {
+  __shared__ uint4 img[4 * 512];
+  const uint32_t l = threadIdx.x & 63u, r = l >> 3, pc = l & 7u;
+  const uint32_t sbase = lds_offset(img + (threadIdx.x >> 6) * 512);
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
+  const uint32_t wa = sbase + (l << 7) + (((l >> 1) & 7u) << 4);
+  const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
+  const uint32_t lo0 = (r << 7) + ((pc ^ (r >> 1)) << 4);  // load voffset
+  const uint32_t so = (r << 7) + (pc << 4);                 // store voffset
+  const uint64_t units_per_block = a.msg_len >> 13;
+  for (uint64_t u = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); u < n_units;
+       u += uint64_t(gridDim.x) * 4) {
+    const uint64_t off = u << 13;
+    const uint64_t j = u / units_per_block;  // bigblob block (wave-uniform)
+    const uint32_t ctr0 = uint32_t((u - j * units_per_block) << 7) + 2 * l;
+    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.src) + off, 0, 8192u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dst =
+        __builtin_amdgcn_make_buffer_rsrc(a.ctext + off, 0, 8192u, 0x00020000);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image free again
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          src, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
+          16, (k & 1) ? (lo0 ^ 64u) : lo0, 1024u * k, 0, 0);
+    const uint32_t *dp = reinterpret_cast<const uint32_t *>(a.refs + j * 64 + 32);
+    uint32_t key[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) key[i] = __builtin_amdgcn_readfirstlane(dp[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u32x4 v[8];
+    const uint32_t w = opaque(wa);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      v[i] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(i) << 4));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t x[16];
+      chacha_block(x, key, ctr0 + h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u32x4 c = v[4 * h + q];
+        c.x ^= x[4 * q];
+        c.y ^= x[4 * q + 1];
+        c.z ^= x[4 * q + 2];
+        c.w ^= x[4 * q + 3];
+        *reinterpret_cast<lds_u32x4 *>(w ^ (uint32_t(4 * h + q) << 4)) = c;
+      }
+    }
+    const uint32_t r0 = opaque(rb), r1 = r0 ^ 64u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32x4 c = *reinterpret_cast<const lds_u32x4 *>(((k & 1) ? r1 : r0) + 1024u * k);
+      __builtin_amdgcn_raw_buffer_store_b128(c, dst, so, 1024u * k, 0);
+    }
   }
 }
 
@@ -1010,8 +1095,24 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
   a.last_len = last_len;
   a.n = n;
   a.refs = const_cast<uint8_t *>(refs);
-  const uint64_t kbs = ((n - 1) * bs + last_len + 63) >> 6;
-  uint64_t grid = (kbs + 255) / 256;
+  const uint64_t total = (n - 1) * bs + last_len;
+  const uint64_t kbs = (total + 63) >> 6;
+  // bulk: whole 8 KiB units through the line kernel (uniform DEK per wave)
+  uint64_t units = 0;
+  if (bs % 8192 == 0 && ((reinterpret_cast<uintptr_t>(ctext) |
+                          reinterpret_cast<uintptr_t>(ptext)) & 15) == 0)
+    units = total >> 13;
+  if (units) {
+    uint64_t grid = (units + 3) / 4;
+    if (grid > 16384) grid = 16384;
+    hipLaunchKernelGGL(k_decrypt_lines, dim3(uint32_t(grid)), dim3(256), 0, s, a,
+                       units);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  a.stride = units << 7;  // first keystream block left for k_decrypt
+  if (a.stride >= kbs) return hipSuccess;
+  uint64_t grid = (kbs - a.stride + 255) / 256;
   if (grid > 65536) grid = 65536;
   hipLaunchKernelGGL(k_decrypt, dim3(uint32_t(grid)), dim3(256), 0, s, a);
   return hipGetLastError();

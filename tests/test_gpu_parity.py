@@ -468,9 +468,55 @@ def test_post_blobs_device_config4_sample(gpu, O):
         assert rh[64 * i:64 * i + 64] == want, i
 
 
+@pytest.mark.parametrize("ln", [1024, 2048, 4096, 16384])
+def test_post_blobs_dense_vs_scattered(gpu, O, ln):
+    """Densely packed equal blobs take the LDS-staged wave path of k_small;
+    the same blobs at permuted offsets take the per-lane path.  Every root
+    and every ctext byte must agree (and sampled roots with the oracle), with
+    and without ctext, with a partial last wave."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    n = 64 * 5 + 17
+    rng = random.Random(ln)
+    perm = list(range(n))
+    rng.shuffle(perm)
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    a = dev_bytes(torch, n * ln, seed=ln)
+    pi = torch.tensor(perm, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    b[:n * ln].view(n, ln)[pi] = a[:n * ln].view(n, ln)
+    torch.cuda.synchronize()
+    lens = torch.full((n,), ln, dtype=torch.int64, device="cuda")
+
+    def run(src, offs, with_ct):
+        roots = zeros(torch, 64 * n)
+        ct = zeros(torch, n * ln) if with_ct else None
+        N.check(N.lib.glfsx_post_blobs_device(2 << 20, blob_salt, None, src.data_ptr(),
+                                              offs.data_ptr(), lens.data_ptr(), n, ln,
+                                              ct.data_ptr() if with_ct else None,
+                                              roots.data_ptr(), None))
+        torch.cuda.synchronize()
+        return host(roots, 64 * n), (host(ct, n * ln) if with_ct else None)
+
+    dense = torch.arange(n, dtype=torch.int64, device="cuda") * ln
+    ra, ca = run(a, dense, True)
+    rb, cb = run(b, pi * ln, True)
+    assert ra == rb
+    assert all(ca[i * ln:(i + 1) * ln] == cb[perm[i] * ln:(perm[i] + 1) * ln]
+               for i in range(n))
+    assert run(a, dense, False)[0] == ra
+    data = host(a, n * ln)
+    for i in [0, 63, 64, n - 1] + rng.sample(range(n), 4):
+        want, _, _, posts = O.create(data[i * ln:(i + 1) * ln], 2 << 20, salt=blob_salt)
+        assert ra[64 * i:64 * i + 64] == want, i
+        assert ca[i * ln:(i + 1) * ln] == posts[0][3], i
+
+
 # ---------------------------------------------------------------- read side
 @pytest.mark.parametrize("bs,size", [(1 << 20, (9 << 20) + 77), (4096, 4096 * 33 + 5),
-                                     (128, 128 * 7)])
+                                     (128, 128 * 7), (8192, 8192 * 3 + 100),
+                                     (8192, 8192 * 5), (65536, 65536 * 2 + 8191),
+                                     (2 << 20, (2 << 20) + 8192 + 64)])
 def test_decrypt_batch_roundtrip(gpu, O, bs, size):
     """getF (ref.go:113-126): decrypting every posted data block with its DEK
     gives back the plaintext; block 0 also checked against the oracle."""
@@ -488,8 +534,15 @@ def test_decrypt_batch_roundtrip(gpu, O, bs, size):
                                              pt.data_ptr(), None))
     torch.cuda.synchronize()
     assert torch.equal(pt[:size], t[:size])
+    assert not pt[size:].any()   # nothing written past the end
     r0 = host(refs, 64)
     assert O.chacha20_xor(host(ct, min(bs, size)), r0[32:]) == host(t, min(bs, size))
+    # unaligned destination: the bulk line kernel is bypassed, same bytes
+    pt2 = zeros(torch, size + 64)
+    N.check(N.lib.glfsx_decrypt_batch_device(ct.data_ptr(), size, bs, refs.data_ptr(),
+                                             pt2.data_ptr() + 1, None))
+    torch.cuda.synchronize()
+    assert torch.equal(pt2[1:size + 1], t[:size])
 
 
 # ------------------------------------------------- writer pipeline, extremes
