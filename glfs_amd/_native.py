@@ -62,6 +62,7 @@ SIGNATURES = {
     "glfsx_version": (_CP, []),
     "glfsx_set_split_target": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),
+    "glfsx_post": (_INT, [_CP, _VP, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch_device": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP, _VP]),
     "glfsx_dek_batch_device": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP]),

@@ -280,6 +280,19 @@ class Machine:
         self.traverse(store, root, lambda cid: not exists_unit(dst, cid),
                       lambda level, ref: dst.add(ref.cid))
 
+    def post(self, store: WO, salt: Optional[bytes], data: bytes,
+             cid_key: Optional[bytes] = None) -> Ref:
+        """ref.go:98-111 post: DEK = DeriveKey(salt, ptext), ctext =
+        ChaCha20(DEK) ^ ptext, CID = the store's hash of ctext -- all on the
+        GPU -- then store.Post(ctext).  A store error propagates."""
+        data = bytes(data)
+        ref = ctypes.create_string_buffer(REF_SIZE)
+        ct = ctypes.create_string_buffer(max(len(data), 1))
+        N.check(N.lib.glfsx_post(_salt_arg(salt) or bytes(32), data, len(data), ct, ref,
+                                 cid_key))
+        store.post(ct.raw[:len(data)], ref.raw, KIND_DATA)
+        return Ref.from_bytes(ref.raw)
+
     def new_writer(self, store: WO, salt: Optional[bytes] = None,
                    cid_key: Optional[bytes] = None) -> Writer:
         """blob.go:85-114."""
@@ -377,6 +390,14 @@ class CIDSet:
         self.cids.add(cid)
 
 
+class ErrNotFound(KeyError):
+    """blobcache.ErrNotFound{CID} [ext]: Get of a CID the store lacks."""
+
+    def __init__(self, cid: bytes):
+        super().__init__(f"blob not found: {cid.hex()}")
+        self.cid = cid
+
+
 class MemStore:
     """In-memory stand-in for blobcache's schema.MemStore [ext].  It keeps
     (CID -> ctext) as posted by the GPU path (a pre-hashed Post: the CID was
@@ -403,7 +424,14 @@ class MemStore:
         return cid in self.blobs
 
     def get(self, cid: bytes) -> bytes:
-        return self.blobs[cid]
+        try:
+            return self.blobs[cid]
+        except KeyError:
+            raise ErrNotFound(cid) from None
+
+    def delete(self, cids) -> None:
+        for cid in cids:
+            self.blobs.pop(cid, None)
 
 
 def crypto_xor(dek: bytes, data: bytes) -> bytes:

@@ -623,6 +623,37 @@ int glfsx_cid_batch_device(const void *d_ptext, uint64_t total,
   return 0;
 }
 
+int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
+               void *ctext_out, uint8_t *ref_out, const uint8_t *cid_key) {
+  if (!salt || !ref_out || (n && !ptext)) return fail(GLFSX_E_ARG, "null argument");
+  if (n > kMaxMsgLen)
+    return fail(GLFSX_E_UNSUPPORTED, "message of %llu bytes above the kernels' limit %llu",
+                (unsigned long long)n, (unsigned long long)kMaxMsgLen);
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  if (int e = c->d_in.ensure(n + 64)) return e;
+  if (int e = c->d_ct.ensure(n + 64)) return e;
+  if (int e = c->d_refs.ensure(64)) return e;
+  if (n)
+    HIP_TRY(hipMemcpyAsync(c->d_in.p, ptext, n, hipMemcpyHostToDevice, c->stream));
+  PostJob j{};  // one message; n == 0 is the empty message (one empty chunk)
+  j.src = c->d_in.u8();
+  j.ctext = c->d_ct.u8();
+  j.stride = 0;
+  j.msg_len = n;
+  j.last_len = n;
+  j.n = 1;
+  j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+  words_from_key(j.salt, salt);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, c->stream));
+  HIP_TRY(hipMemcpyAsync(ref_out, c->d_refs.p, 64, hipMemcpyDeviceToHost, c->stream));
+  if (ctext_out && n)
+    HIP_TRY(hipMemcpyAsync(ctext_out, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int glfsx_post_batch(const uint8_t salt[32], const void *ptext, uint64_t total,
                      uint64_t block_size, void *ctext_out, uint8_t *refs_out,
                      const uint8_t *cid_key) {

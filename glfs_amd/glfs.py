@@ -145,6 +145,29 @@ class Machine:
             raise ValueError(f"blob exceeds max size {max_size}")
         return r.read()
 
+    def sync(self, dst, src, x: Ref) -> None:
+        """sync.go:14-39 Sync: copy everything x references from src into dst;
+        a tree's entries are synced (from the tree bytes bigblob's Sync hands
+        over) before the tree blob itself; nothing happens when dst already
+        has the root."""
+        if x.type == TYPE_BLOB:
+            self.bbag.sync(dst, src, x.root, lambda r: None)
+        elif x.type == TYPE_TREE:
+            from .tree import read_tree_bytes
+
+            def sync_entries(r):
+                for ent in read_tree_bytes(r.read()):
+                    self.sync(dst, src, ent.ref)
+
+            self.bbag.sync(dst, src, x.root, sync_entries)
+        else:
+            raise ValueError(f"can't sync unrecognized type {x.type}")
+
+    def get_at_path(self, store, ref: Ref, subpath: str) -> Ref:
+        """tree.go:91-99 GetAtPath (ErrNoEnt when nothing is at subpath)."""
+        from .tree import get_at_path
+        return get_at_path(store, ref, subpath)
+
     # ---------------------------------------------------------------- trees
     def new_tree_writer(self, store, **kw):
         """tree.go:290-298."""
@@ -194,3 +217,43 @@ def post_blob(store, r) -> Ref:
 def post_blobs(store, blobs) -> list:
     """Batched PostBlob on the default machine (see Machine.post_blobs)."""
     return _default_machine().post_blobs(store, blobs)
+
+
+def sync(dst, src, x: Ref) -> None:
+    """sync.go:14 on the default machine."""
+    _default_machine().sync(dst, src, x)
+
+
+def get_at_path(store, ref: Ref, subpath: str) -> Ref:
+    """tree.go:91 on the default machine."""
+    return _default_machine().get_at_path(store, ref, subpath)
+
+
+def post_tree(store, ents) -> Ref:
+    """tree.go:195 PostTree on the default machine."""
+    return _default_machine().post_tree(store, ents)
+
+
+def post_tree_slice(store, ents) -> Ref:
+    """tree.go:240 PostTreeSlice on the default machine."""
+    return _default_machine().post_tree_slice(store, ents)
+
+
+def post_tree_map(store, m: dict) -> Ref:
+    """tree.go:250 PostTreeMap on the default machine."""
+    return _default_machine().post_tree_map(store, m)
+
+
+def get_tree_slice(store, ref: Ref, max_ents: int = 10 ** 6) -> list:
+    """tree.go:137 GetTreeSlice on the default machine."""
+    return _default_machine().get_tree_slice(store, ref, max_ents)
+
+
+def new_blob_writer(store) -> TypedWriter:
+    """blob.go:37-39 NewBlobWriter on the default machine."""
+    return _default_machine().new_blob_writer(store)
+
+
+def get_blob(store, x: Ref) -> bigblob.Reader:
+    """blob.go:20-22 GetBlob on the default machine."""
+    return _default_machine().get_blob(store, x)

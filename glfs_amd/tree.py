@@ -37,6 +37,19 @@ class TreeError(ValueError):
     """The errors tree.go returns with fmt.Errorf / errors.New."""
 
 
+class ErrNoEnt(KeyError):
+    """errors.go:8-14 ErrNoEnt{Name}."""
+
+    def __init__(self, name: str):
+        super().__init__(f"no entry at {name}")
+        self.name = name
+
+
+def is_err_no_ent(err: BaseException) -> bool:
+    """errors.go:16-18."""
+    return isinstance(err, ErrNoEnt)
+
+
 @dataclass(frozen=True)
 class TreeEntry:
     """tree.go:74-78 TreeEntry{Name, FileMode, Ref}."""
@@ -303,3 +316,27 @@ def get_tree_slice(store, ref: glfs.Ref, max_ents: int = 10 ** 6,
         raise TreeError(f"wrong ref type: have {ref.type} want {glfs.TYPE_TREE}")
     ents = read_tree_bytes(bigblob.read_all(store, ref.root), cid_from_json)
     return ents[:max_ents]
+
+
+def lookup_path(store, ent: TreeEntry, subpath: str,
+                cid_from_json=_cid_from_json) -> TreeEntry:
+    """tree.go:101-133 Lookup: walk subpath one name at a time through the
+    (GPU-decrypted) tree blobs; entries are sorted, so a scan stops at the
+    first name past the wanted one."""
+    subpath = subpath.strip("/")
+    if subpath == "":
+        return ent
+    if ent.ref.type != glfs.TYPE_TREE:
+        raise TreeError("can only take subpath of type tree")
+    head, _, rest = subpath.partition("/")
+    for e in get_tree_slice(store, ent.ref, 1 << 62, cid_from_json):
+        if e.name == head:
+            return lookup_path(store, e, rest, cid_from_json)
+        if _name_key(e.name) > _name_key(head):
+            break
+    raise ErrNoEnt(head)
+
+
+def get_at_path(store, ref: glfs.Ref, subpath: str, cid_from_json=_cid_from_json) -> glfs.Ref:
+    """tree.go:91-99 GetAtPath."""
+    return lookup_path(store, TreeEntry("", 0, ref), subpath, cid_from_json).ref

@@ -10,6 +10,8 @@
  *
  * Reference interfaces replaced (reference = blobcache/glfs, Go):
  *   glfsx_derive_key       bigblob/ref.go:152-161  DeriveKey(out, salt, input)
+ *   glfsx_post             bigblob/ref.go:98-111   (*Machine).post, one message,
+ *                          minus the store.Post call
  *   glfsx_post_batch*,     bigblob/ref.go:98-111   (*Machine).post, batched over
  *   glfsx_dek/cid_batch_device
  *                          equal-size blocks, minus the store.Post call
@@ -95,6 +97,13 @@ uint32_t glfsx_set_split_target(uint32_t wgs);
  * (<= 32) bytes of the XOF. */
 int glfsx_derive_key(uint8_t *out, size_t out_len, const uint8_t salt[32],
                      const void *input, size_t n);
+
+/* ref.go:98-111 (*Machine).post of ONE message of n bytes (n may be 0: the
+ * empty blob's post(indexSalt, nil), blob.go:187-189), host buffers, minus
+ * the store.Post call: writes the 64-byte ref (CID||DEK) and, if ctext_out is
+ * non-NULL, the n bytes of ctext.  cid_key as for glfsx_post_batch. */
+int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
+               void *ctext_out, uint8_t *ref_out, const uint8_t *cid_key);
 
 /* ref.go:98 post() for ceil(total/block_size) blocks of `ptext` (the last one
  * short), host buffers.  refs_out: 64 bytes per block.  ctext_out nullable.
