@@ -13,7 +13,8 @@ and rank 0 builds the root.
 Prints ONE JSON line (rank 0).  Extra objects: roofline (dominant kernel,
 HIP events on the launch stream), cpu_baseline (the oracle on host cores),
 host_round_trip (host memory -> GPU -> host ctext + refs), valu (second
-roofline).  Data is synthetic: splitmix64 stream (oracle_fill_splitmix).
+roofline).  Data is synthetic: a splitmix64 byte stream generated on the GPU
+(glfsx_fill_splitmix_device).  Only the cpu_baseline leg touches oracle/.
 """
 from __future__ import annotations
 
@@ -311,8 +312,8 @@ def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=5):
     """BASELINE config 4's hashing: 1M distinct 4 KiB blobs (glfs.PostBlob with
     the blob type salt, bs = 2 MiB), device-resident, one lane per blob
     (glfsx_post_blobs_device).  Reported beside the headline, not as it."""
-    from oracle import oracle as O  # only to derive the blob type salt's bytes
-    blob_salt = O.derive_key(bytes(32), b"blob")
+    from glfs_amd import glfs
+    blob_salt = glfs.Machine().make_salt("blob")   # machine.go:50-54, on the GPU
     with torch.cuda.stream(stream):
         data = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
         ct = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
@@ -345,12 +346,16 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     n = int(args.host_rt_gib * GIB) // bs * bs
     if n == 0:
         return None
+    import torch
     host = np.empty(n, dtype=np.uint8)
-    from oracle import oracle as O
-    O.lib().oracle_fill_splitmix(host.ctypes.data, 0, min(n, 64 * MIB), args.seed)
-    reps = n // (64 * MIB)
-    for i in range(1, reps):
-        host[i * 64 * MIB:(i + 1) * 64 * MIB] = host[:64 * MIB]
+    # the same splitmix stream, generated on the GPU and copied down
+    dev = torch.empty(64 * MIB, dtype=torch.uint8, device="cuda")
+    for off in range(0, n, 64 * MIB):
+        m = min(64 * MIB, n - off)
+        N.check(N.lib.glfsx_fill_splitmix_device(dev.data_ptr(), off, m, args.seed, None))
+        torch.cuda.synchronize()
+        host[off:off + m] = dev[:m].cpu().numpy()
+    del dev
     counts = (ctypes.c_uint64 * 2)()
     sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)   # native sink, no Python per block
     root = N.glfsx_root()

@@ -840,7 +840,10 @@ void glfsx_writer_free(glfsx_writer *w) {
     tls_stream_pool.push_back({w->c->dev, w->s_up, w->ws, w->s_down});
   } else {
     for (hipStream_t st : {w->s_up, w->ws, w->s_down})
-      if (st) (void)hipStreamDestroy(st);
+      if (st) {
+        release_stream_scratch(st);
+        (void)hipStreamDestroy(st);
+      }
   }
   delete w;
 }

@@ -23,6 +23,8 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #ifndef GLFSX_LDS_CTEXT
 #define GLFSX_LDS_CTEXT 1
@@ -774,67 +776,83 @@ __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
   }
 }
 
-// Read side, bulk: one wave per 8 KiB of ctext (lane l = 128-B line l = two
-// keystream blocks), bs % 8192 == 0 so the wave's DEK is uniform (SGPRs; the
-// key-only quarter-rounds of round 1 are hoisted by the compiler).  Lines
-// arrive by buffer_load ... lds (8 full lines per instruction) into the
-// swizzled image of k_pass, each lane takes its line, XORs the keystream,
-// writes it back in place, and the wave stores 8 full lines per instruction.
-// Covers whole 8 KiB units [0, a.n_units); k_decrypt does the rest.
-__global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units) {
+// Read side, bulk: one wave per 4 KiB unit of ctext (lane l = keystream
+// block l of the unit), bs % 4096 == 0 so the unit's DEK is uniform (scalar
+// loads into SGPRs; the key-only quarter-rounds of round 1 are hoisted by the
+// compiler).  Each wave has two 4 KiB images: unit u+stride arrives by
+// buffer_load ... lds (4 instructions x 8 full 128-B lines) while unit u is
+// decrypted.  Image layout: piece p (16 B) of lane L's block sits at
+// 64L + 16 (p ^ ((L >> 2) & 3)), so the lane's ds_read_b128s are conflict-free
+// and the loader / storer lane l of instruction k touches image byte
+// 1024k + 16l <-> unit byte 1024k + vo(l).  Covers units [0, n_units);
+// k_decrypt does the rest.
+__global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units,
+                                                       uint32_t upb_shift) {
   __shared__ uint4 img[4 * 512];
-  const uint32_t l = threadIdx.x & 63u, r = l >> 3, pc = l & 7u;
-  const uint32_t sbase = lds_offset(img + (threadIdx.x >> 6) * 512);
-  const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
-  const uint32_t wa = sbase + (l << 7) + (((l >> 1) & 7u) << 4);
-  const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
-  const uint32_t lo0 = (r << 7) + ((pc ^ (r >> 1)) << 4);  // load voffset
-  const uint32_t so = (r << 7) + (pc << 4);                 // store voffset
-  const uint64_t units_per_block = a.msg_len >> 13;
-  for (uint64_t u = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); u < n_units;
-       u += uint64_t(gridDim.x) * 4) {
-    const uint64_t off = u << 13;
-    const uint64_t j = u / units_per_block;  // bigblob block (wave-uniform)
-    const uint32_t ctr0 = uint32_t((u - j * units_per_block) << 7) + 2 * l;
+  const uint32_t l = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wbase = lds_offset(img + wv * 512);
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(wbase);
+  const uint32_t vo = ((l >> 2) << 6) + (((l & 3u) ^ ((l >> 4) & 3u)) << 4);
+  const uint32_t wa = wbase + (l << 6) + (((l >> 2) & 3u) << 4);
+  const uint32_t rl = wbase + (l << 4);  // linear slot for the stores
+  const uint64_t upb = a.msg_len >> 12;  // units per bigblob block
+  const uint64_t stride = uint64_t(gridDim.x) * 4;
+  auto issue = [&](uint64_t uu, uint32_t buf) {
     const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.src) + off, 0, 8192u, 0x00020000);
-    const __amdgpu_buffer_rsrc_t dst =
-        __builtin_amdgcn_make_buffer_rsrc(a.ctext + off, 0, 8192u, 0x00020000);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image free again
+        const_cast<uint8_t *>(a.src) + (uu << 12), 0, 4096u, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < 4; ++k)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          src, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
-          16, (k & 1) ? (lo0 ^ 64u) : lo0, 1024u * k, 0, 0);
-    const uint32_t *dp = reinterpret_cast<const uint32_t *>(a.refs + j * 64 + 32);
+          src, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 4096u * buf + 1024u * k),
+          16, vo, 1024u * k, 0, 0);
+  };
+  uint64_t u = uint64_t(blockIdx.x) * 4 + wv;
+  if (u < n_units) issue(u, 0);
+  for (uint32_t buf = 0; u < n_units; u += stride, buf ^= 1u) {
+    const uint64_t un = u + stride;
+    // the other image was last read by the previous unit's store ds_reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool more = un < n_units;
+    if (more) issue(un, buf ^ 1u);
+    // bigblob block (uniform): its DEK.  upb_shift = log2(units per block)
+    // when that is a power of two (no 64-bit scalar division per unit)
+    const uint64_t j = upb_shift < 64 ? u >> upb_shift : u / upb;
+    const __attribute__((address_space(4))) uint32_t *kp =
+        (const __attribute__((address_space(4))) uint32_t *)(uintptr_t)(
+            a.refs + j * 64 + 32);
     uint32_t key[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) key[i] = __builtin_amdgcn_readfirstlane(dp[i]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    u32x4 v[8];
-    const uint32_t w = opaque(wa);
+    for (int i = 0; i < 8; ++i) key[i] = kp[i];
+    // this unit's lines: all but the 4 youngest vector-memory ops (the next
+    // unit's loads) are done -- the previous unit's stores included
+    if (more)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t w = opaque(wa) + 4096u * buf;
+    u32x4 v[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      v[i] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(i) << 4));
+    for (int q = 0; q < 4; ++q)
+      v[q] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(q) << 4));
+    uint32_t x[16];
+    chacha_block(x, key, uint32_t((u - j * upb) << 6) + l);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint32_t x[16];
-      chacha_block(x, key, ctr0 + h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        u32x4 c = v[4 * h + q];
-        c.x ^= x[4 * q];
-        c.y ^= x[4 * q + 1];
-        c.z ^= x[4 * q + 2];
-        c.w ^= x[4 * q + 3];
-        *reinterpret_cast<lds_u32x4 *>(w ^ (uint32_t(4 * h + q) << 4)) = c;
-      }
+    for (int q = 0; q < 4; ++q) {
+      u32x4 c = v[q];
+      c.x ^= x[4 * q];
+      c.y ^= x[4 * q + 1];
+      c.z ^= x[4 * q + 2];
+      c.w ^= x[4 * q + 3];
+      *reinterpret_cast<lds_u32x4 *>(w ^ (uint32_t(q) << 4)) = c;
     }
-    const uint32_t r0 = opaque(rb), r1 = r0 ^ 64u;
+    const __amdgpu_buffer_rsrc_t dst =
+        __builtin_amdgcn_make_buffer_rsrc(a.ctext + (u << 12), 0, 4096u, 0x00020000);
+    const uint32_t r0 = opaque(rl) + 4096u * buf;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const u32x4 c = *reinterpret_cast<const lds_u32x4 *>(((k & 1) ? r1 : r0) + 1024u * k);
-      __builtin_amdgcn_raw_buffer_store_b128(c, dst, so, 1024u * k, 0);
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 c = *reinterpret_cast<const lds_u32x4 *>(r0 + 1024u * k);
+      __builtin_amdgcn_raw_buffer_store_b128(c, dst, vo, 1024u * k, 0);
     }
   }
 }
@@ -910,23 +928,54 @@ uint32_t split_target_default() {
 std::atomic<uint32_t> g_split_target{split_target_default()};
 constexpr uint32_t kMaxSplitLog2 = 6;  // k_merge merges <= 64 subtrees
 
-// Stream-ordered scratch for split mode (a few bytes per workgroup).  The
-// device pool keeps freed blocks (release threshold = max), so steady-state
-// allocations are pool hits, not hipMalloc calls.
-hipError_t scratch_alloc(uint32_t **p, size_t bytes, hipStream_t s) {
-  static std::atomic<uint64_t> pools_done{0};
+// Split-mode scratch (32 B per workgroup): one persistent buffer per
+// (device, stream), reused by every launch on that stream -- launches on one
+// stream are ordered, so the buffer is never shared by two in flight.  The
+// stream-ordered pool (hipMallocAsync / hipFreeAsync per launch) serialised
+// the Writer's three-stream pipeline (host round trip 43.5 -> 24 GiB/s).
+// A buffer only grows when the split target is raised at run time; the old
+// one is released after its stream drains.
+struct ScratchSlot {
+  int dev;
+  hipStream_t stream;
+  uint32_t *p;
+  size_t bytes;
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchSlot> g_scratch;
+
+hipError_t scratch_get(uint32_t **p, size_t bytes, hipStream_t s) {
+  std::mutex &mu = g_scratch_mu;
+  std::vector<ScratchSlot> &slots = g_scratch;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 64 && !(pools_done.load() & (1ull << dev))) {
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t thr = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  std::lock_guard<std::mutex> lk(mu);
+  for (ScratchSlot &sl : slots) {
+    if (sl.dev != dev || sl.stream != s) continue;
+    if (sl.bytes >= bytes) {
+      *p = sl.p;
+      return hipSuccess;
     }
-    pools_done.fetch_or(1ull << dev);
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    (void)hipFree(sl.p);
+    sl.p = nullptr;
+    sl.bytes = 0;
+    e = hipMalloc(reinterpret_cast<void **>(&sl.p), bytes);
+    if (e != hipSuccess) return e;
+    sl.bytes = bytes;
+    *p = sl.p;
+    return hipSuccess;
   }
-  return hipMallocAsync(reinterpret_cast<void **>(p), bytes, s);
+  // at least the default target's worst case, so it never needs to grow
+  const size_t want = bytes > (size_t(2) << 16) ? bytes : (size_t(2) << 16);
+  uint32_t *q = nullptr;
+  e = hipMalloc(reinterpret_cast<void **>(&q), want);
+  if (e != hipSuccess) return e;
+  slots.push_back({dev, s, q, want});
+  *p = q;
+  return hipSuccess;
 }
 
 template <bool CHACHA>
@@ -946,7 +995,7 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
   a.split_log2 = sl;
   a.scratch = nullptr;
   if (sl) {
-    hipError_t e = scratch_alloc(&a.scratch, size_t(a.n << sl) * 32, s);
+    hipError_t e = scratch_get(&a.scratch, size_t(a.n << sl) * 32, s);
     if (e != hipSuccess) return e;
   }
   hipError_t e;
@@ -959,10 +1008,6 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
     case 32: e = launch_g<32, CHACHA>(a, aligned, s); break;
     case 64: e = launch_g<64, CHACHA>(a, aligned, s); break;
     default: e = hipErrorInvalidValue;
-  }
-  if (a.scratch) {
-    hipError_t f = hipFreeAsync(a.scratch, s);
-    if (e == hipSuccess) e = f;
   }
   return e;
 }
@@ -1012,6 +1057,21 @@ void words_from_key(uint32_t w[8], const uint8_t key[32]) {
 }
 
 uint32_t set_split_target(uint32_t wgs) { return g_split_target.exchange(wgs); }
+
+void release_stream_scratch(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (size_t i = 0; i < g_scratch.size(); ++i) {
+    if (g_scratch[i].stream != s) continue;
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess && cur == g_scratch[i].dev)
+      (void)hipFree(g_scratch[i].p);
+    else
+      continue;  // another device's stream of the same handle value
+    g_scratch[i] = g_scratch.back();
+    g_scratch.pop_back();
+    --i;
+  }
+}
 
 void blake3_iv_words(uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) w[i] = kIV[i];
@@ -1097,20 +1157,23 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
   a.refs = const_cast<uint8_t *>(refs);
   const uint64_t total = (n - 1) * bs + last_len;
   const uint64_t kbs = (total + 63) >> 6;
-  // bulk: whole 8 KiB units through the line kernel (uniform DEK per wave)
+  // bulk: whole 4 KiB units through the line kernel (uniform DEK per unit)
   uint64_t units = 0;
-  if (bs % 8192 == 0 && ((reinterpret_cast<uintptr_t>(ctext) |
+  if (bs % 4096 == 0 && ((reinterpret_cast<uintptr_t>(ctext) |
                           reinterpret_cast<uintptr_t>(ptext)) & 15) == 0)
-    units = total >> 13;
+    units = total >> 12;
   if (units) {
     uint64_t grid = (units + 3) / 4;
     if (grid > 16384) grid = 16384;
+    const uint64_t upb = bs >> 12;
+    const uint32_t upb_shift =
+        (upb & (upb - 1)) == 0 ? uint32_t(__builtin_ctzll(upb)) : 64u;
     hipLaunchKernelGGL(k_decrypt_lines, dim3(uint32_t(grid)), dim3(256), 0, s, a,
-                       units);
+                       units, upb_shift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  a.stride = units << 7;  // first keystream block left for k_decrypt
+  a.stride = units << 6;  // first keystream block left for k_decrypt
   if (a.stride >= kbs) return hipSuccess;
   uint64_t grid = (kbs - a.stride + 255) / 256;
   if (grid > 65536) grid = 65536;

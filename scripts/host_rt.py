@@ -10,6 +10,12 @@ sys.path.insert(0, ".")
 from glfs_amd import _native as N  # noqa: E402
 
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 4
+hold = float(sys.argv[2]) if len(sys.argv) > 2 else 0   # GiB held by torch's allocator
+if hold:
+    import torch
+    held = [torch.empty(int(hold * (1 << 30)), dtype=torch.uint8, device="cuda")]
+    if len(sys.argv) > 3 and sys.argv[3] == "free":
+        del held
 bs = 1 << 20
 n = int(gib * (1 << 30)) // bs * bs
 host = np.ones(n, dtype=np.uint8)
