@@ -422,6 +422,53 @@ def test_large_blob_properties(gpu, O):
     assert host(refs, 64 * n0) == rh
 
 
+def test_config3_64gib_every_ref(gpu, O):
+    """BASELINE config 3 at its full size (the bench workload): a 64 GiB
+    device-resident blob at 1 MiB blocks, splitmix seed 3.  Every one of the
+    65536 data refs and every ctext byte against the threaded oracle (1 GiB
+    at a time, ptext copied down from HBM), then the two index levels and
+    the root rebuilt by the oracle from those refs (blob.go:165-206)."""
+    torch = _torch()
+    import numpy as np
+    from glfs_amd import _native as N
+    size, bs, seed = 64 * GIB, MIB, 3
+    n0, bf = size // bs, bs // 64
+    raw = O.derive_key(bytes(32), b"raw")
+    idx = O.derive_key(bytes(32), b"index")
+    free, _ = torch.cuda.mem_get_info()
+    if free < 2 * size + GIB:
+        pytest.skip(f"needs {2 * size + GIB} B of HBM, {free} free")
+    t = dev_bytes(torch, size, seed=seed)
+    ct = torch.empty(size, dtype=torch.uint8, device="cuda")
+    root, posts = _create_device(torch, bs, t, size, ct)
+    refs = zeros(torch, 64 * n0)
+    N.check(N.lib.glfsx_post_batch_device(raw, t.data_ptr(), size, bs, None,
+                                          refs.data_ptr(), None, None))
+    torch.cuda.synchronize()
+    got_refs = host(refs, 64 * n0)
+    L = O.lib()
+    piece = GIB
+    want_refs = np.empty(64 * (piece // bs), dtype=np.uint8)
+    want_ct = np.empty(piece, dtype=np.uint8)
+    for off in range(0, size, piece):
+        pt = t[off:off + piece].cpu().numpy()
+        L.oracle_post_batch(want_refs.ctypes.data, want_ct.ctypes.data, raw,
+                            pt.ctypes.data, piece, bs, None, 16)
+        j0 = off // bs
+        assert got_refs[64 * j0:64 * (j0 + piece // bs)] == want_refs.tobytes(), off
+        assert np.array_equal(ct[off:off + piece].cpu().numpy(), want_ct), off
+    del t, ct
+    torch.cuda.empty_cache()
+    level = got_refs
+    while len(level) > 64:
+        level = b"".join(O.post(idx, level[i:i + bs].ljust(bs, b"\0"))[0]
+                         for i in range(0, len(level), 64 * bf))
+    assert root == level
+    assert posts == n0 + 4 + 1
+    # the root bench.py prints for this workload
+    assert root[:32].hex().startswith("e87d3dc4ad171bce")
+
+
 # ------------------------------------------------------------- small blobs
 def test_post_blobs_vs_oracle(gpu, O):
     """Batched glfs.PostBlob (config 4 shape): every root, every Post, in order,
