@@ -71,7 +71,61 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 
-#define B3G(a, b, c, d, x, y) \
+// ARX steps as single-instruction asm statements (GLFSX_ASM_ARX): same
+// instructions as the C form, but the compiler schedules them as opaque
+// units, which on gfx950 issues measurably faster (DESIGN.md "Rooflines",
+// tools/arx.hip).  Used from the second round on, so round 1 keeps the C
+// form's constant folding (IV literals, uniform key words).
+#ifndef GLFSX_ASM_ARX
+#define GLFSX_ASM_ARX 1
+#endif
+template <int N>
+__device__ __forceinline__ uint32_t rotr_a(uint32_t x) {
+  uint32_t d;
+  asm("v_alignbit_b32 %0, %1, %1, %2" : "=v"(d) : "v"(x), "i"(N));
+  return d;
+}
+__device__ __forceinline__ uint32_t xor_a(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_xor_b32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t add_a(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_add_u32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t add3_a(uint32_t a, uint32_t b, uint32_t c) {
+#if GLFSX_ASM_ARX == 2
+  return add_a(add_a(a, b), c);
+#else
+  uint32_t d;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+#endif
+}
+
+#define B3G_A(a, b, c, d, x, y)       \
+  a = add3_a(a, b, (x));              \
+  d = rotr_a<16>(xor_a(d, a));        \
+  c = add_a(c, d);                    \
+  b = rotr_a<12>(xor_a(b, c));        \
+  a = add3_a(a, b, (y));              \
+  d = rotr_a<8>(xor_a(d, a));         \
+  c = add_a(c, d);                    \
+  b = rotr_a<7>(xor_a(b, c));
+
+#define CQR_A(a, b, c, d)             \
+  a = add_a(a, b);                    \
+  d = rotr_a<16>(xor_a(d, a));        \
+  c = add_a(c, d);                    \
+  b = rotr_a<20>(xor_a(b, c));        \
+  a = add_a(a, b);                    \
+  d = rotr_a<24>(xor_a(d, a));        \
+  c = add_a(c, d);                    \
+  b = rotr_a<25>(xor_a(b, c));
+
+#define B3G_C(a, b, c, d, x, y) \
   a = a + b + (x);            \
   d = rotr(d ^ a, 16);        \
   c = c + d;                  \
@@ -80,6 +134,17 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
   d = rotr(d ^ a, 8);         \
   c = c + d;                  \
   b = rotr(b ^ c, 7);
+
+#if GLFSX_ASM_ARX
+#define B3G(a, b, c, d, x, y)           \
+  if constexpr (R == 0) {               \
+    B3G_C(a, b, c, d, x, y)             \
+  } else {                              \
+    B3G_A(a, b, c, d, x, y)             \
+  }
+#else
+#define B3G(a, b, c, d, x, y) B3G_C(a, b, c, d, x, y)
+#endif
 
 template <int R>
 __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
@@ -142,8 +207,27 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
   x[13] = 0;
   x[14] = 0;
   x[15] = 0;
+  // round 1 in C: its key-only quarter-rounds are uniform and hoisted
+  CQR(x[0], x[4], x[8], x[12]);
+  CQR(x[1], x[5], x[9], x[13]);
+  CQR(x[2], x[6], x[10], x[14]);
+  CQR(x[3], x[7], x[11], x[15]);
+  CQR(x[0], x[5], x[10], x[15]);
+  CQR(x[1], x[6], x[11], x[12]);
+  CQR(x[2], x[7], x[8], x[13]);
+  CQR(x[3], x[4], x[9], x[14]);
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 1; i < 10; ++i) {
+#if GLFSX_ASM_ARX
+    CQR_A(x[0], x[4], x[8], x[12]);
+    CQR_A(x[1], x[5], x[9], x[13]);
+    CQR_A(x[2], x[6], x[10], x[14]);
+    CQR_A(x[3], x[7], x[11], x[15]);
+    CQR_A(x[0], x[5], x[10], x[15]);
+    CQR_A(x[1], x[6], x[11], x[12]);
+    CQR_A(x[2], x[7], x[8], x[13]);
+    CQR_A(x[3], x[4], x[9], x[14]);
+#else
     CQR(x[0], x[4], x[8], x[12]);
     CQR(x[1], x[5], x[9], x[13]);
     CQR(x[2], x[6], x[10], x[14]);
@@ -152,6 +236,7 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
     CQR(x[1], x[6], x[11], x[12]);
     CQR(x[2], x[7], x[8], x[13]);
     CQR(x[3], x[4], x[9], x[14]);
+#endif
   }
   x[0] += c0;
   x[1] += c1;

@@ -1,0 +1,42 @@
+"""Secondary legs alone, for per-kernel profiling (rocprofv3 PMC passes):
+config 4's small-blob kernels (bench.small_blobs) and the read side
+(batched getF decrypt over a --gib GiB blob at 1 MiB blocks).
+usage: python scripts/legs.py [small|read|both] [--gib G]"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "both"
+    gib = float(sys.argv[sys.argv.index("--gib") + 1]) if "--gib" in sys.argv else 16
+    import torch
+    from glfs_amd import _native as N
+    torch.cuda.set_device(0)
+    N.set_device(0)
+    stream = torch.cuda.Stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    out = {}
+    if what in ("small", "both"):
+        out["small_blobs"] = bench.small_blobs(torch, N, stream, sp)
+    if what in ("read", "both"):
+        bs = bench.MIB
+        per = int(gib * bench.GIB) // bs * bs
+        with torch.cuda.stream(stream):
+            data = torch.empty(per, dtype=torch.uint8, device="cuda")
+            ct = torch.empty(per, dtype=torch.uint8, device="cuda")
+            N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), 0, per, 3, sp))
+        stream.synchronize()
+        roof, _ = bench.roofline(torch, N, data, ct, per, bs, stream, sp)
+        out["read_side"] = roof["read_side"]
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
