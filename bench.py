@@ -30,11 +30,22 @@ sys.path.insert(0, ROOT)
 
 GIB, MIB = 1 << 30, 1 << 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# int-VALU roofline (DESIGN.md "Rooflines"): gfx950 issues the 3-input integer
-# ops this path lives on (v_add3_u32, v_alignbit_b32) at 16 lanes/clk/SIMD and
-# mixed ARX streams at ~4 cycles per wave64 instruction (tools/opbench.hip,
-# tools/gmix2.hip): 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
-VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+# int-VALU roofline (DESIGN.md "Rooflines").  gfx950 issues wave64 integer
+# ops in two classes (tools/mix.hip): full rate, 2 cycles (v_add_u32,
+# v_xor_b32, v_lshrrev_b32, v_bitop3_b32, VGPR/literal operands) and half
+# rate, 4 cycles (v_add3_u32, v_alignbit_b32, v_perm_b32, v_lshlrev_b32, any
+# SGPR operand).  The ideal time of a kernel is its algorithmic instruction
+# mix at those costs on 1024 SIMDs at the 2.4 GHz peak clock:
+#   BLAKE3 G  = 6 full (2 add, 4 xor) + 6 half (2 add3, 4 alignbit) = 36 cyc
+#   ChaCha QR = 8 full (4 add, 4 xor) + 4 half (4 alignbit)          = 32 cyc
+#   compression = 56 G + 8 xor; one parent per 16 blocks (1 MiB, G = 4)
+#   ChaCha block = 80 QR - 3 uniform QRs (hoisted) + 16 xor + 5 full adds
+#                  + 8 half adds (SGPR key words)
+SIMDS, PEAK_GHZ = 1024, 2.4
+_COMPRESS = 56 * 36 + 8 * 2
+_CHACHA = (80 - 3) * 32 + 16 * 2 + 5 * 2 + 8 * 4
+IDEAL_CYCLES_PER_BLOCK = {"dek": _COMPRESS * (1 + 1 / 16),
+                          "cid": _CHACHA + _COMPRESS * (1 + 1 / 16)}
 # VALU lane-instructions per plaintext byte, measured with rocprofv3
 # SQ_INSTS_VALU x 64 / bytes (profiles/r1/summary.json).
 INSTR_PER_BYTE = {"dek": 11.60, "cid": 26.53}
@@ -253,12 +264,17 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             "algorithmic_bytes_per_launch": alg[dom],
             "avg_ms": {k: round(v, 4) for k, v in avg.items()},
             "hashed_GBps": {k: round(per / (v * 1e-3) / 1e9, 1) for k, v in avg.items()}}
-    ops = {k: INSTR_PER_BYTE[k] * per for k in avg}
-    valu = {"bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_PEAK_TOPS, 2),
-            "instr_per_byte": INSTR_PER_BYTE,
-            "achieved": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12, 2) for k in avg},
-            "frac": {k: round(ops[k] / (avg[k] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 3)
-                     for k in avg}}
+    # ideal: each wave-cycle of a SIMD covers 64 lanes x 64 B blocks
+    ideal_ms = {k: IDEAL_CYCLES_PER_BLOCK[k] * (per / 4096) / (SIMDS * PEAK_GHZ * 1e9) * 1e3
+                for k in avg}
+    valu = {"bound": "valu", "unit": "ms per launch",
+            "model": "class-weighted issue: full-rate ops 2 cyc, half-rate 4 cyc per wave64 "
+                     "instruction, 1024 SIMDs at 2.4 GHz (DESIGN.md Rooflines)",
+            "ideal_cycles_per_64B_block": {k: round(v, 1) for k, v in IDEAL_CYCLES_PER_BLOCK.items()},
+            "ideal_ms": {k: round(v, 3) for k, v in ideal_ms.items()},
+            "achieved_ms": {k: round(v, 3) for k, v in avg.items()},
+            "frac": {k: round(ideal_ms[k] / avg[k], 3) for k in avg},
+            "instr_per_byte": INSTR_PER_BYTE}
     del refs
     roof["read_side"] = read
     return roof, valu

@@ -28,11 +28,13 @@ template <int N> __device__ __forceinline__ uint32_t rotr_c(uint32_t x) {
 template <int N> __device__ __forceinline__ uint32_t rotr_ab(uint32_t x) {
   uint32_t d; asm("v_alignbit_b32 %0, %1, %1, %2" : "=v"(d) : "v"(x), "i"(N)); return d; }
 template <int V> __device__ __forceinline__ uint32_t R16(uint32_t x) {
-  return (V == 0 || V == 4) ? rotr_c<16>(x) : V == 1 ? rotr_lo<16>(x) : V == 5 ? rotr_ab<16>(x) : rot16_pk(x); }
+  return (V == 0 || V == 4) ? rotr_c<16>(x) : V == 1 ? rotr_lo<16>(x) : (V == 5 || V == 9) ? rotr_ab<16>(x) : rot16_pk(x); }
 template <int V, int N> __device__ __forceinline__ uint32_t R(uint32_t x) {
-  return (V == 0 || V == 3 || V == 4) ? rotr_c<N>(x) : V == 5 ? rotr_ab<N>(x) : rotr_lo<N>(x); }
+  return (V == 0 || V == 3 || V == 4) ? rotr_c<N>(x) : (V == 5 || V == 9) ? rotr_ab<N>(x) : rotr_lo<N>(x); }
+__device__ __forceinline__ uint32_t add3a(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d; asm("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c)); return d; }
 template <int V> __device__ __forceinline__ uint32_t A3(uint32_t a, uint32_t b, uint32_t c) {
-  return (V == 0 || V == 3) ? a + b + c : add2(add2(a, b), c); }
+  return (V == 0 || V == 3) ? a + b + c : V == 9 ? add3a(a, b, c) : add2(add2(a, b), c); }
 template <int V> __device__ __forceinline__ uint32_t A2(uint32_t a, uint32_t b) {
   return (V == 0 || V == 3) ? a + b : add2(a, b); }
 template <int V> __device__ __forceinline__ uint32_t X(uint32_t a, uint32_t b) {
@@ -145,14 +147,15 @@ __global__ __launch_bounds__(256) void k_chacha(uint32_t *out, uint32_t iters) {
 }
 
 typedef void (*Kf)(uint32_t *, uint32_t);
+static int g_lds = 0;  // dynamic LDS per block: limits blocks (= waves per SIMD) per CU
 static double run(const char *name, Kf k, uint32_t *out, int grid, uint32_t iters,
                   double units, int instr_per_unit, uint32_t *ref) {
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, out, iters); CK(hipDeviceSynchronize());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), g_lds, 0, out, iters); CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   float best = 1e30f;
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, out, iters);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), g_lds, 0, out, iters);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (ms < best) best = ms;
   }
@@ -163,8 +166,8 @@ static double run(const char *name, Kf k, uint32_t *out, int grid, uint32_t iter
   if (ref) { CK(hipMemcpy(hr, ref, n * 4, hipMemcpyDeviceToHost)); ok = memcmp(h, hr, n * 4) == 0; }
   const double waves_per_simd = double(grid) * 4 / 1024;
   const double ns = best * 1e6 / (waves_per_simd * iters * units);
-  printf("%-16s grid %6d  %8.3f ms  %7.3f ns/unit/SIMD = %5.1f cyc at 2.1 GHz  (%d instr: %.2f cyc/instr)  %s\n",
-         name, grid, best, ns, ns * 2.1, instr_per_unit, ns * 2.1 / instr_per_unit,
+  printf("lds %6d %-16s grid %6d  %8.3f ms  %7.3f ns/unit/SIMD = %5.1f cyc at 2.1 GHz  (%d instr: %.2f cyc/instr)  %s\n",
+         g_lds, name, grid, best, ns, ns * 2.1, instr_per_unit, ns * 2.1 / instr_per_unit,
          ref ? (ok ? "match" : "MISMATCH") : "ref");
   return best;
 }
@@ -173,7 +176,10 @@ int main() {
   uint32_t *out[3];
   for (auto &o : out) CK(hipMalloc(&o, size_t(4) << 22));
   const uint32_t it = 256;
-  for (int grid : {4096, 16384}) {
+  for (int lds : {0, 40960, 20480}) {
+  g_lds = lds;
+  for (int grid : {16384}) {
+    run("blake_asm_add3", k_blake<9>, out[1], grid, it, 32, 12, nullptr);
     run("blake_c", k_blake<0>, out[0], grid, it, 32, 12, nullptr);
     run("blake_fast", k_blake<1>, out[1], grid, it, 32, 18, out[0]);
     run("blake_fast_pk", k_blake<2>, out[2], grid, it, 32, 17, out[0]);
@@ -188,6 +194,7 @@ int main() {
     run("chacha_blk4", k_chacha<8>, out[1], grid, it, 32, 12, out[0]);
     run("chacha_fast", k_chacha<1>, out[1], grid, it, 32, 16, out[0]);
     run("chacha_fast_pk", k_chacha<2>, out[2], grid, it, 32, 15, out[0]);
+  }
   }
   return 0;
 }
