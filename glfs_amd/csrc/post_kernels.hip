@@ -137,7 +137,7 @@ __device__ __forceinline__ uint32_t add3_a(uint32_t a, uint32_t b, uint32_t c) {
 
 #if GLFSX_ASM_ARX
 #define B3G(a, b, c, d, x, y)           \
-  if constexpr (R == 0) {               \
+  if constexpr (R == 0 || !A) {         \
     B3G_C(a, b, c, d, x, y)             \
   } else {                              \
     B3G_A(a, b, c, d, x, y)             \
@@ -146,7 +146,7 @@ __device__ __forceinline__ uint32_t add3_a(uint32_t a, uint32_t b, uint32_t c) {
 #define B3G(a, b, c, d, x, y) B3G_C(a, b, c, d, x, y)
 #endif
 
-template <int R>
+template <int R, bool A = true>
 __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
                                          const uint32_t (&m)[16]) {
   constexpr const int *s = kSched.s[R];
@@ -163,6 +163,7 @@ __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
 // cv <- first 8 words of compress(cv, m, counter, block_len, flags): the
 // chaining value, or for a ROOT compression the first 32 output bytes
 // (XOF block 0), which is all the write path ever reads.
+template <bool A = true>
 __device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
                                             const uint32_t (&m)[16],
                                             uint32_t ctr_lo, uint32_t ctr_hi,
@@ -170,13 +171,13 @@ __device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
   uint32_t v[16] = {cv[0],  cv[1],  cv[2],  cv[3],  cv[4],  cv[5],
                     cv[6],  cv[7],  kIV[0], kIV[1], kIV[2], kIV[3],
                     ctr_lo, ctr_hi, blen,   flags};
-  b3_round<0>(v, m);
-  b3_round<1>(v, m);
-  b3_round<2>(v, m);
-  b3_round<3>(v, m);
-  b3_round<4>(v, m);
-  b3_round<5>(v, m);
-  b3_round<6>(v, m);
+  b3_round<0, A>(v, m);
+  b3_round<1, A>(v, m);
+  b3_round<2, A>(v, m);
+  b3_round<3, A>(v, m);
+  b3_round<4, A>(v, m);
+  b3_round<5, A>(v, m);
+  b3_round<6, A>(v, m);
 #pragma unroll
   for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
 }
@@ -192,6 +193,7 @@ __device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
   b = rotr(b ^ c, 25);
 
 // RFC 8439 block function, nonce 0^12 (ref.go:138), 32-bit block counter.
+template <bool A = true>
 __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
                                              const uint32_t (&k)[8],
                                              uint32_t ctr) {
@@ -219,6 +221,7 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
 #pragma unroll
   for (int i = 1; i < 10; ++i) {
 #if GLFSX_ASM_ARX
+   if constexpr (A) {
     CQR_A(x[0], x[4], x[8], x[12]);
     CQR_A(x[1], x[5], x[9], x[13]);
     CQR_A(x[2], x[6], x[10], x[14]);
@@ -227,6 +230,16 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
     CQR_A(x[1], x[6], x[11], x[12]);
     CQR_A(x[2], x[7], x[8], x[13]);
     CQR_A(x[3], x[4], x[9], x[14]);
+   } else {
+    CQR(x[0], x[4], x[8], x[12]);
+    CQR(x[1], x[5], x[9], x[13]);
+    CQR(x[2], x[6], x[10], x[14]);
+    CQR(x[3], x[7], x[11], x[15]);
+    CQR(x[0], x[5], x[10], x[15]);
+    CQR(x[1], x[6], x[11], x[12]);
+    CQR(x[2], x[7], x[8], x[13]);
+    CQR(x[3], x[4], x[9], x[14]);
+   }
 #else
     CQR(x[0], x[4], x[8], x[12]);
     CQR(x[1], x[5], x[9], x[13]);
@@ -323,7 +336,7 @@ struct KArgs {
 
 // Merge step after the last block of local chunk jj: pop/parent/push on the
 // lane's CV stack (eager merges = ctz(jj+1); final merges empty the stack).
-template <int D>
+template <int D, bool A = true>
 __device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
                                            uint32_t (&stk)[D > 0 ? D : 1][8],
                                            uint32_t &depth, uint32_t jj,
@@ -347,7 +360,7 @@ __device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
       --depth;
       const uint32_t fl =
           base | kParent | ((whole && last && depth == 0) ? kRoot : 0u);
-      b3_compress(cv, m, 0u, 0u, 64u, fl);
+      b3_compress<A>(cv, m, 0u, 0u, 64u, fl);
     }
     if (!last) {
 #pragma unroll
@@ -383,7 +396,7 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   return x;
 }
 
-template <bool CHACHA, bool STAGE = false>
+template <bool CHACHA, bool STAGE = false, bool A = true>
 __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
                                            const uint4 &w1, const uint4 &w2,
                                            const uint4 &w3, uint32_t chunk,
@@ -395,7 +408,7 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
                     w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
   if constexpr (CHACHA) {
     uint32_t x[16];
-    chacha_block(x, dek, (chunk << 4) + b);
+    chacha_block<A>(x, dek, (chunk << 4) + b);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] ^= x[i];
     if (STAGE) {  // LDS staging: wa = this lane's swizzled line address
@@ -411,7 +424,7 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
       out[3] = make_uint4(m[12], m[13], m[14], m[15]);
     }
   }
-  b3_compress(cv, m, chunk, 0u, 64u, fl);
+  b3_compress<A>(cv, m, chunk, 0u, 64u, fl);
 }
 
 // Fast path: the lane's G chunks are all full (16*G consecutive 64-B blocks,
@@ -420,7 +433,7 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
 // next even block's before the odd one, so HBM latency is covered and no
 // buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
 // the chaining-value reset are per-chunk (scalar), not per-block selects.
-template <int G, bool CHACHA, bool STAGE = false>
+template <int G, bool CHACHA, bool STAGE = false, bool A = true>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
@@ -507,7 +520,7 @@ __device__ __forceinline__ void lane_subtree_full(
         b3 = nb[3];
       }
       constexpr bool stg = CHACHA && STAGE;
-      full_block<CHACHA, stg>(cv, a0, a1, a2, a3, chunk, 2 * pp,
+      full_block<CHACHA, stg, A>(cv, a0, a1, a2, a3, chunk, 2 * pp,
                          base | (pp == 0 ? kChunkStart : 0u), dek,
                          cq && !stg ? cq + 4 * blk : nullptr, wst, 0);
       if (!gl && blk + 2 < NB) {
@@ -519,7 +532,7 @@ __device__ __forceinline__ void lane_subtree_full(
       }
       uint32_t fl = base;
       if (pp == 7) fl |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
-      full_block<CHACHA, stg>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
+      full_block<CHACHA, stg, A>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
                          cq && !stg ? cq + 4 * (blk + 1) : nullptr, wst, 1);
       if (stg) {
         // lane l stores piece pc of line 8k + r: each store instruction
@@ -539,7 +552,7 @@ __device__ __forceinline__ void lane_subtree_full(
         }
       }
     }
-    lane_merge<D>(cv, stk, depth, jj, jj + 1 == uint32_t(G), whole, key, base);
+    lane_merge<D, A>(cv, stk, depth, jj, jj + 1 == uint32_t(G), whole, key, base);
   }
 }
 
@@ -547,7 +560,7 @@ __device__ __forceinline__ void lane_subtree_full(
 // its chaining value in cv (or the root output when `whole`: this lane holds
 // the entire message).  Eager merges after chunk jj = ctz(jj+1), final merges
 // right to left: the same tree as BLAKE3's incremental hasher.
-template <int G, bool CHACHA, bool ALIGNED>
+template <int G, bool CHACHA, bool ALIGNED, bool A = true>
 __device__ __forceinline__ void lane_subtree(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint64_t len,
     uint32_t first, uint32_t n_my, bool whole, const uint32_t (&key)[8],
@@ -572,7 +585,7 @@ __device__ __forceinline__ void lane_subtree(
       load_block<ALIGNED>(m, msg + coff + boff, avail);
       if constexpr (CHACHA) {
         uint32_t x[16];
-        chacha_block(x, dek, (chunk << 4) + b);
+        chacha_block<A>(x, dek, (chunk << 4) + b);
 #pragma unroll
         for (int i = 0; i < 16; ++i) m[i] ^= x[i];
         if (avail < 64) mask_tail(m, avail);
@@ -584,9 +597,9 @@ __device__ __forceinline__ void lane_subtree(
         fl |= kChunkEnd;
         if (whole && n_my == 1) fl |= kRoot;
       }
-      b3_compress(cv, m, chunk, 0u, avail < 64 ? avail : 64u, fl);
+      b3_compress<A>(cv, m, chunk, 0u, avail < 64 ? avail : 64u, fl);
     }
-    lane_merge<D>(cv, stk, depth, jj, last, whole, key, base);
+    lane_merge<D, A>(cv, stk, depth, jj, last, whole, key, base);
   }
 }
 
@@ -643,7 +656,9 @@ __device__ __forceinline__ void tree_reduce(uint32_t *lds, uint32_t k,
   }
 }
 
-template <int G, bool CHACHA, bool ALIGNED>
+// A: ARX in the asm form (many waves per SIMD); false: the compiler's form,
+// which issues faster when a launch leaves a SIMD one or two waves
+template <int G, bool CHACHA, bool ALIGNED, bool A = true>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   // one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext
   // in the CHACHA pass, plaintext in the DEK pass): 40 KiB, 4 WGs per CU
@@ -701,14 +716,14 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   const bool wave_fast = __ballot(fast) == ~0ull;
   if (fast) {
     if (kStageU4 && wave_fast && (cmsg || !CHACHA))  // wave-uniform
-      lane_subtree_full<G, CHACHA, kStageU4 != 0>(
+      lane_subtree_full<G, CHACHA, kStageU4 != 0, A>(
           cv, msg, cmsg, first, whole, key, a.base, dek,
           lds_offset(lds_u4 + 512 + (t >> 6) * 512), uint32_t(len), cbase);
     else
-      lane_subtree_full<G, CHACHA>(cv, msg, cmsg, first, whole, key, a.base,
-                                   dek, 0u, 0u, cbase);
+      lane_subtree_full<G, CHACHA, false, A>(cv, msg, cmsg, first, whole, key,
+                                             a.base, dek, 0u, 0u, cbase);
   } else if (n_my) {
-    lane_subtree<G, CHACHA, ALIGNED>(cv, msg, cmsg, len, first, n_my, whole,
+    lane_subtree<G, CHACHA, ALIGNED, A>(cv, msg, cmsg, len, first, n_my, whole,
                                      key, a.base, dek, cbase);
   }
   if (whole) {  // uniform: depends on len only; lane 0 holds the root output
@@ -871,6 +886,7 @@ __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
 // and the loader / storer lane l of instruction k touches image byte
 // 1024k + 16l <-> unit byte 1024k + vo(l).  Covers units [0, n_units);
 // k_decrypt does the rest.
+template <bool A>
 __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units,
                                                        uint32_t upb_shift) {
   __shared__ uint4 img[4 * 512];
@@ -921,7 +937,7 @@ __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units
     for (int q = 0; q < 4; ++q)
       v[q] = *reinterpret_cast<const lds_u32x4 *>(w ^ (uint32_t(q) << 4));
     uint32_t x[16];
-    chacha_block(x, key, uint32_t((u - j * upb) << 6) + l);
+    chacha_block<A>(x, key, uint32_t((u - j * upb) << 6) + l);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       u32x4 c = v[q];
@@ -989,10 +1005,17 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, uint64_t offset,
   }
 }
 
+constexpr uint32_t kLatencyWGs = 512;
+
 template <int G, bool CHACHA>
 hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
   const dim3 grid(uint32_t(a.n << a.split_log2)), block(256);
-  if (aligned)
+  // <= 2 waves per SIMD (512 workgroups of 4 waves on 1024 SIMDs): the
+  // compiler-scheduled ARX issues faster than the asm form (tools/arx.hip)
+  const bool lat = grid.x <= kLatencyWGs;
+  if (aligned && lat)
+    hipLaunchKernelGGL((k_pass<G, CHACHA, true, false>), grid, block, 0, s, a);
+  else if (aligned)
     hipLaunchKernelGGL((k_pass<G, CHACHA, true>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL((k_pass<G, CHACHA, false>), grid, block, 0, s, a);
@@ -1253,8 +1276,12 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
     const uint64_t upb = bs >> 12;
     const uint32_t upb_shift =
         (upb & (upb - 1)) == 0 ? uint32_t(__builtin_ctzll(upb)) : 64u;
-    hipLaunchKernelGGL(k_decrypt_lines, dim3(uint32_t(grid)), dim3(256), 0, s, a,
-                       units, upb_shift);
+    if (grid <= kLatencyWGs)
+      hipLaunchKernelGGL(k_decrypt_lines<false>, dim3(uint32_t(grid)), dim3(256), 0, s,
+                         a, units, upb_shift);
+    else
+      hipLaunchKernelGGL(k_decrypt_lines<true>, dim3(uint32_t(grid)), dim3(256), 0, s,
+                         a, units, upb_shift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -33,10 +33,10 @@ __global__ __launch_bounds__(256) void k_valu(uint32_t *out, uint32_t iters) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = threadIdx.x * 16 + i;
   for (uint32_t it = 0; it < iters; ++it) {
-    B3G(v[0], v[4], v[8], v[12], it, v[1]);
-    B3G(v[1], v[5], v[9], v[13], v[2], it);
-    B3G(v[2], v[6], v[10], v[14], it, v[3]);
-    B3G(v[3], v[7], v[11], v[15], v[0], it);
+    B3G_A(v[0], v[4], v[8], v[12], it, v[1]);
+    B3G_A(v[1], v[5], v[9], v[13], v[2], it);
+    B3G_A(v[2], v[6], v[10], v[14], it, v[3]);
+    B3G_A(v[3], v[7], v[11], v[15], v[0], it);
   }
   uint32_t x = 0;
 #pragma unroll
