@@ -1086,9 +1086,9 @@ hipError_t scratch_get(uint32_t **p, size_t bytes, hipStream_t s) {
   return hipSuccess;
 }
 
-template <bool CHACHA>
-hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
-                       hipStream_t s) {
+// Chunks per lane (g) and log2 workgroups per message (sl) of a launch over
+// n messages of at most maxlen bytes.
+void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   const uint64_t C = maxlen ? (maxlen + 1023) >> 10 : 1;
   int g = 1;
   while (256ull * g < C) g *= 2;
@@ -1096,10 +1096,20 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
   // message until the launch fills the chip (256 CUs x 8 workgroups)
   uint32_t sl = 0;
   const uint64_t target = g_split_target.load(std::memory_order_relaxed);
-  while (g > 1 && sl < kMaxSplitLog2 && (a.n << sl) < target) {
+  while (g > 1 && sl < kMaxSplitLog2 && (n << sl) < target) {
     g /= 2;
     ++sl;
   }
+  *g_out = g;
+  *sl_out = sl;
+}
+
+template <bool CHACHA>
+hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
+                       hipStream_t s) {
+  int g;
+  uint32_t sl;
+  pass_plan(a.n, maxlen, &g, &sl);
   a.split_log2 = sl;
   a.scratch = nullptr;
   if (sl) {
@@ -1212,6 +1222,31 @@ hipError_t launch_cid_pass(const PostJob &job, hipStream_t s) {
   a.out_off = 0;
   const uint64_t maxlen = job.n > 1 ? std::max(job.msg_len, job.last_len)
                                     : job.last_len;
+  int g;
+  uint32_t sl;
+  pass_plan(job.n, maxlen, &g, &sl);
+  // Latency-bound launches (index nodes, single posts, small batches): the
+  // fused pass leaves one wave per SIMD running ChaCha20 and BLAKE3 in
+  // series.  The keystream has no chaining, so instead every 64-B block gets
+  // its own lane (the read side's kernels: ctext = ptext ^ ChaCha20(DEK_j)),
+  // and the CID is a BLAKE3 pass over the ctext like the DEK pass.  Needs
+  // the ctext in memory, DEKs in dense slots, contiguous messages.
+  const bool dense = job.out.bf >= job.n;
+  const bool contiguous = job.n == 1 || job.stride == job.msg_len;
+  if ((job.n << sl) <= kLatencyWGs && job.ctext && dense && contiguous &&
+      (job.n == 1 || job.msg_len % 64 == 0)) {
+    const uint64_t bs = job.n > 1 ? job.msg_len
+                                  : std::max<uint64_t>(4096, (job.last_len + 4095) & ~4095ull);
+    hipError_t e = launch_decrypt(job.src, job.ctext, job.n, bs, job.last_len,
+                                  job.out.refs, s);
+    if (e != hipSuccess) return e;
+    KArgs b = a;
+    b.src = job.ctext;
+    b.ctext = nullptr;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(job.ctext) |
+                           uintptr_t(job.stride)) & 15) == 0;
+    return launch_pass<false>(b, maxlen, aligned, s);
+  }
   return launch_pass<true>(a, maxlen, is_aligned(job), s);
 }
 
