@@ -21,3 +21,7 @@ if [ -x tools/kbench ]; then
   timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_BUSY_CYCLES --kernel-trace -f csv -d $OUT/kb -o run -- tools/kbench 8 > $OUT/kb.log 2>&1
 fi
 python scripts/prof_summary.py $OUT $OUT/summary.json > $OUT/summary.txt
+# secondary legs (config 4 small blobs, read side) alone: legs/
+#   bash scripts/profile_legs.sh gpurun_out/prof_legs
+# per-launch HBM traffic for bench.py's roofline.traffic:
+#   python scripts/pmc_traffic.py profiles/r1/summary.json profiles/pmc_traffic.json
