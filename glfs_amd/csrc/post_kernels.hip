@@ -888,7 +888,8 @@ __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
 // k_decrypt does the rest.
 template <bool A>
 __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units,
-                                                       uint32_t upb_shift) {
+                                                       uint32_t upb_shift,
+                                                       uint32_t run_shift) {
   __shared__ uint4 img[4 * 512];
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -898,7 +899,11 @@ __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units
   const uint32_t wa = wbase + (l << 6) + (((l >> 2) & 3u) << 4);
   const uint32_t rl = wbase + (l << 4);  // linear slot for the stores
   const uint64_t upb = a.msg_len >> 12;  // units per bigblob block
-  const uint64_t stride = uint64_t(gridDim.x) * 4;
+  // the wave walks runs of R = 2^run_shift consecutive units inside one
+  // bigblob block (R divides the units per block): the DEK and its key-only
+  // quarter-rounds are loop-invariant over a run
+  const uint64_t n_runs = (n_units + (1ull << run_shift) - 1) >> run_shift;
+  const uint64_t wstride = uint64_t(gridDim.x) * 4;
   auto issue = [&](uint64_t uu, uint32_t buf) {
     const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.src) + (uu << 12), 0, 4096u, 0x00020000);
@@ -908,23 +913,28 @@ __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units
           src, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 4096u * buf + 1024u * k),
           16, vo, 1024u * k, 0, 0);
   };
-  uint64_t u = uint64_t(blockIdx.x) * 4 + wv;
-  if (u < n_units) issue(u, 0);
-  for (uint32_t buf = 0; u < n_units; u += stride, buf ^= 1u) {
-    const uint64_t un = u + stride;
-    // the other image was last read by the previous unit's store ds_reads
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bool more = un < n_units;
-    if (more) issue(un, buf ^ 1u);
+  uint64_t run = uint64_t(blockIdx.x) * 4 + wv;
+  if (run < n_runs) issue(run << run_shift, 0);
+  uint32_t buf = 0;
+  for (; run < n_runs; run += wstride) {
+    const uint64_t u0 = run << run_shift;
+    const uint64_t u1 = min(u0 + (1ull << run_shift), n_units);
     // bigblob block (uniform): its DEK.  upb_shift = log2(units per block)
-    // when that is a power of two (no 64-bit scalar division per unit)
-    const uint64_t j = upb_shift < 64 ? u >> upb_shift : u / upb;
+    // when that is a power of two (no 64-bit scalar division per run)
+    const uint64_t j = upb_shift < 64 ? u0 >> upb_shift : u0 / upb;
     const __attribute__((address_space(4))) uint32_t *kp =
         (const __attribute__((address_space(4))) uint32_t *)(uintptr_t)(
             a.refs + j * 64 + 32);
     uint32_t key[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) key[i] = kp[i];
+    const uint64_t nrun = run + wstride;
+   for (uint64_t u = u0; u < u1; ++u, buf ^= 1u) {
+    const uint64_t un = u + 1 < u1 ? u + 1 : (nrun << run_shift);
+    // the other image was last read by the previous unit's store ds_reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool more = u + 1 < u1 || nrun < n_runs;
+    if (more) issue(un, buf ^ 1u);
     // this unit's lines: all but the 4 youngest vector-memory ops (the next
     // unit's loads) are done -- the previous unit's stores included
     if (more)
@@ -955,6 +965,7 @@ __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units
       const u32x4 c = *reinterpret_cast<const lds_u32x4 *>(r0 + 1024u * k);
       __builtin_amdgcn_raw_buffer_store_b128(c, dst, vo, 1024u * k, 0);
     }
+   }
   }
 }
 
@@ -1306,17 +1317,24 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
                           reinterpret_cast<uintptr_t>(ptext)) & 15) == 0)
     units = total >> 12;
   if (units) {
-    uint64_t grid = (units + 3) / 4;
-    if (grid > 16384) grid = 16384;
     const uint64_t upb = bs >> 12;
     const uint32_t upb_shift =
         (upb & (upb - 1)) == 0 ? uint32_t(__builtin_ctzll(upb)) : 64u;
+    // runs of 2^run_shift units per wave (inside one block), as long as
+    // there are still >= 65536 runs: the grid (<= 16384 workgroups of 4
+    // waves) stays as fine-grained as with one unit per step
+    uint32_t run_shift = 0;
+    if (upb_shift < 64)
+      while (run_shift < upb_shift && (units >> (run_shift + 1)) >= 65536) ++run_shift;
+    const uint64_t runs = (units + (1ull << run_shift) - 1) >> run_shift;
+    uint64_t grid = (runs + 3) / 4;
+    if (grid > 16384) grid = 16384;
     if (grid <= kLatencyWGs)
       hipLaunchKernelGGL(k_decrypt_lines<false>, dim3(uint32_t(grid)), dim3(256), 0, s,
-                         a, units, upb_shift);
+                         a, units, upb_shift, run_shift);
     else
       hipLaunchKernelGGL(k_decrypt_lines<true>, dim3(uint32_t(grid)), dim3(256), 0, s,
-                         a, units, upb_shift);
+                         a, units, upb_shift, run_shift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
