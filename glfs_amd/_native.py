@@ -61,6 +61,7 @@ SIGNATURES = {
     "glfsx_set_device": (_INT, [_INT]),
     "glfsx_version": (_CP, []),
     "glfsx_set_split_target": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "glfsx_set_latency_wgs": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),
     "glfsx_post": (_INT, [_CP, _VP, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP]),
@@ -139,6 +140,12 @@ def device_count() -> int:
 
 def set_device(dev: int) -> None:
     check(lib.glfsx_set_device(dev))
+
+
+def set_latency_wgs(wgs: int) -> int:
+    """Tuning knob (include/glfsx.h): launches of at most `wgs` workgroups
+    use the latency-mode kernels.  Returns the previous value."""
+    return lib.glfsx_set_latency_wgs(wgs)
 
 
 def set_split_target(wgs: int) -> int:

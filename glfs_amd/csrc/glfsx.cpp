@@ -525,6 +525,7 @@ const char *glfsx_last_error(void) { return tls_err.c_str(); }
 const char *glfsx_version(void) { return "glfsx 0.1 gfx950"; }
 
 uint32_t glfsx_set_split_target(uint32_t wgs) { return set_split_target(wgs); }
+uint32_t glfsx_set_latency_wgs(uint32_t wgs) { return set_latency_wgs(wgs); }
 
 int glfsx_device_count(void) {
   int n = 0;

@@ -79,6 +79,9 @@ hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
 // workgroups spreads each message over up to 64 workgroups.  0 disables it.
 // Returns the previous value.
 uint32_t set_split_target(uint32_t wgs);
+// Latency-mode threshold in workgroups (see post_kernels.hip); returns the
+// previous value.
+uint32_t set_latency_wgs(uint32_t wgs);
 // Drop the split-mode scratch kept for stream s (call before destroying s,
 // after it has drained).
 void release_stream_scratch(hipStream_t s);

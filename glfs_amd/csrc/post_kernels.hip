@@ -796,7 +796,7 @@ struct SArgs {
   uint32_t out_off;
 };
 
-template <int G, bool CHACHA>
+template <int G, bool CHACHA, bool A = true>
 __global__ __launch_bounds__(256) void k_small(SArgs a) {
   // 4 waves x 8 KiB staging image (same layout as k_pass's)
   __shared__ uint4 lds_u4[4 * 512];
@@ -830,16 +830,16 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
   const bool dense = aligned && len == uint64_t(G) << 10 &&
                      off == o0 + (uint64_t(l) * G << 10) && (!CHACHA || cmsg);
   if (__ballot(dense) == ~0ull) {  // wave-uniform
-    lane_subtree_full<G, CHACHA, true>(
+    lane_subtree_full<G, CHACHA, true, A>(
         cv, a.src + o0, cmsg ? a.ctext + o0 : nullptr, l * G, true, key, a.base,
         dek, lds_offset(lds_u4 + (threadIdx.x >> 6) * 512), 64u * G << 10,
         0u - l * G);
   } else if (aligned && len == uint64_t(G) << 10) {
-    lane_subtree_full<G, CHACHA>(cv, msg, cmsg, 0u, true, key, a.base, dek);
+    lane_subtree_full<G, CHACHA, false, A>(cv, msg, cmsg, 0u, true, key, a.base, dek);
   } else if (aligned) {
-    lane_subtree<G, CHACHA, true>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
+    lane_subtree<G, CHACHA, true, A>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
   } else {
-    lane_subtree<G, CHACHA, false>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
+    lane_subtree<G, CHACHA, false, A>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
   }
   store_digest(ref + a.out_off, cv);
 }
@@ -1016,14 +1016,19 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, uint64_t offset,
   }
 }
 
-constexpr uint32_t kLatencyWGs = 512;
+// Latency mode: launches of at most this many 256-lane workgroups (default
+// 512 = 2 waves per SIMD) run the compiler-scheduled ARX form, and the CID
+// pass splits into a per-block keystream launch + a BLAKE3 pass.
+// glfsx_set_latency_wgs overrides it (tuning, tests of both forms).
+std::atomic<uint32_t> g_latency_wgs{512};
+uint32_t latency_wgs() { return g_latency_wgs.load(std::memory_order_relaxed); }
 
 template <int G, bool CHACHA>
 hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
   const dim3 grid(uint32_t(a.n << a.split_log2)), block(256);
   // <= 2 waves per SIMD (512 workgroups of 4 waves on 1024 SIMDs): the
   // compiler-scheduled ARX issues faster than the asm form (tools/arx.hip)
-  const bool lat = grid.x <= kLatencyWGs;
+  const bool lat = grid.x <= latency_wgs();
   if (aligned && lat)
     hipLaunchKernelGGL((k_pass<G, CHACHA, true, false>), grid, block, 0, s, a);
   else if (aligned)
@@ -1145,7 +1150,19 @@ template <bool CHACHA>
 hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
   const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
-  switch (C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0) {
+  const int gsel = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0;
+  if (grid.x <= latency_wgs()) {  // few blobs: the compiler's ARX form
+    switch (gsel) {
+      case 1: hipLaunchKernelGGL((k_small<1, CHACHA, false>), grid, block, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_small<2, CHACHA, false>), grid, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_small<4, CHACHA, false>), grid, block, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_small<8, CHACHA, false>), grid, block, 0, s, a); break;
+      case 16: hipLaunchKernelGGL((k_small<16, CHACHA, false>), grid, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  switch (gsel) {
     case 1: hipLaunchKernelGGL((k_small<1, CHACHA>), grid, block, 0, s, a); break;
     case 2: hipLaunchKernelGGL((k_small<2, CHACHA>), grid, block, 0, s, a); break;
     case 4: hipLaunchKernelGGL((k_small<4, CHACHA>), grid, block, 0, s, a); break;
@@ -1186,6 +1203,8 @@ void words_from_key(uint32_t w[8], const uint8_t key[32]) {
 }
 
 uint32_t set_split_target(uint32_t wgs) { return g_split_target.exchange(wgs); }
+
+uint32_t set_latency_wgs(uint32_t wgs) { return g_latency_wgs.exchange(wgs); }
 
 void release_stream_scratch(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -1244,7 +1263,7 @@ hipError_t launch_cid_pass(const PostJob &job, hipStream_t s) {
   // the ctext in memory, DEKs in dense slots, contiguous messages.
   const bool dense = job.out.bf >= job.n;
   const bool contiguous = job.n == 1 || job.stride == job.msg_len;
-  if ((job.n << sl) <= kLatencyWGs && job.ctext && dense && contiguous &&
+  if ((job.n << sl) <= latency_wgs() && job.ctext && dense && contiguous &&
       (job.n == 1 || job.msg_len % 64 == 0)) {
     const uint64_t bs = job.n > 1 ? job.msg_len
                                   : std::max<uint64_t>(4096, (job.last_len + 4095) & ~4095ull);
@@ -1329,7 +1348,7 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
     const uint64_t runs = (units + (1ull << run_shift) - 1) >> run_shift;
     uint64_t grid = (runs + 3) / 4;
     if (grid > 16384) grid = 16384;
-    if (grid <= kLatencyWGs)
+    if (grid <= latency_wgs())
       hipLaunchKernelGGL(k_decrypt_lines<false>, dim3(uint32_t(grid)), dim3(256), 0, s,
                          a, units, upb_shift, run_shift);
     else

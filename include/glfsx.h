@@ -91,6 +91,11 @@ const char *glfsx_version(void);
  * it; the default is 2048.  Results are identical either way.  Returns the
  * previous value; process-wide. */
 uint32_t glfsx_set_split_target(uint32_t wgs);
+/* Tuning (no reference counterpart): launches of at most `wgs` workgroups
+ * (default 512, i.e. <= 2 waves per SIMD) use the latency-mode kernels
+ * (compiler-scheduled ARX; CID as keystream launch + BLAKE3 pass).  Results
+ * are identical either way.  Returns the previous value; process-wide. */
+uint32_t glfsx_set_latency_wgs(uint32_t wgs);
 
 /* --- primitives -------------------------------------------------------- */
 /* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input, first out_len

@@ -114,6 +114,64 @@ def split_target():
     N.set_split_target(old)
 
 
+@pytest.fixture
+def latency_wgs():
+    """Restores the latency-mode threshold (include/glfsx.h) after a test."""
+    from glfs_amd import _native as N
+    old = N.set_latency_wgs(512)
+    N.set_latency_wgs(old)
+    yield N.set_latency_wgs
+    N.set_latency_wgs(old)
+
+
+@pytest.mark.parametrize("bs,total", [(1 << 20, (40 << 20) + 77), (65536, 65536 * 600 + 1),
+                                      (4096, 4096 * 3000 + 5), (2 << 20, 2 << 20)])
+def test_arx_forms_vs_oracle(gpu, O, latency_wgs, split_target, bs, total):
+    """Both ARX forms (asm-form kernels for many workgroups, compiler form +
+    split CID pass in latency mode) on the same inputs: refs, ctext, the
+    read-side decrypt and small-blob roots bit-exact with each other and the
+    oracle.  Threshold 0 = never latency mode, 2**31 = always."""
+    torch = _torch()
+    from glfs_amd import _native as N, bigblob, glfs
+    rng = random.Random(total)
+    salt = bytes(rng.randrange(256) for _ in range(32))
+    data = O.fill_splitmix(total, total + 11)
+    blobs = [O.fill_splitmix(n, 7000 + i) for i, n in
+             enumerate([4096] * 300 + [0, 1, 1000, 5000, 16384])]
+    outs, decs, smalls = [], [], []
+    for thr in (0, 1 << 31):
+        latency_wgs(thr)
+        for target in (0, 2048):
+            split_target(target)
+            refs, ct = _post_batch_host(salt, data, bs)
+            outs.append((refs, ct))
+            n0 = (total + bs - 1) // bs
+            assert len(refs) == 64 * n0
+            # read side (getF, batched): back to the plaintext
+            ctd, refd = dev_bytes(torch, total, data=ct), dev_bytes(torch, len(refs), data=refs)
+            pt = zeros(torch, total + 64)
+            N.check(N.lib.glfsx_decrypt_batch_device(ctd.data_ptr(), total, bs,
+                                                     refd.data_ptr(), pt.data_ptr(), None))
+            torch.cuda.synchronize()
+            decs.append(host(pt, total))
+        smalls.append([r.root.ref.marshal_binary() for r in
+                       glfs.Machine().post_blobs(bigblob.MemStore(2 << 20), blobs)])
+    assert all(o == outs[0] for o in outs)
+    assert all(d == data for d in decs)
+    assert smalls[0] == smalls[1]
+    refs, ct = outs[0]
+    n0 = (total + bs - 1) // bs
+    for j in sorted({0, n0 - 1} | set(rng.sample(range(n0), min(3, n0)))):
+        blk = data[j * bs:(j + 1) * bs]
+        r, c = O.post(salt, blk)
+        assert refs[64 * j:64 * j + 64] == r, j
+        assert ct[j * bs:j * bs + len(blk)] == c, j
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    for i in (0, 299, 300, 301, 302, 303, 304):
+        want, _, _, _ = O.create(blobs[i], 2 << 20, salt=blob_salt)
+        assert smalls[0][i] == want, i
+
+
 @pytest.mark.parametrize("bs,total", [(1 << 20, (3 << 20) + 5), (1 << 20, 9 << 20),
                                       (2 << 20, (5 << 20) + 999), (5 << 20, 11 << 20),
                                       (300_000, 2_000_003), (65536, 65536 * 3 + 1),
