@@ -259,8 +259,8 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             traffic = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": {"dek": "k_pass<4,false,true> (keyed BLAKE3, DEK)",
-                       "cid": "k_pass<4,true,true> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
+            "kernel": {"dek": "k_pass<4,false,true,true> (keyed BLAKE3, DEK)",
+                       "cid": "k_pass<4,true,true,true> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
             "algorithmic_bytes_per_launch": alg[dom],
             "avg_ms": {k: round(v, 4) for k, v in avg.items()},
             "hashed_GBps": {k: round(per / (v * 1e-3) / 1e9, 1) for k, v in avg.items()}}
