@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -114,6 +115,22 @@ int ctx_get(Ctx **out) {
   return 0;
 }
 
+// Wait for a stream whose results the caller is about to return.  Polls
+// for up to kSpinNs first: a blocking hipStreamSynchronize wakes the thread
+// tens of microseconds after the GPU finishes, which is most of the host
+// overhead of a short call (a 1 GiB Create takes ~1.3 ms); longer waits block.
+constexpr int64_t kSpinNs = 2000000;
+hipError_t stream_wait(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    if (std::chrono::duration_cast<std::chrono::nanoseconds>(
+            std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+      return hipStreamSynchronize(s);
+  }
+}
+
 hipStream_t pick_stream(Ctx *c, void *stream) {
   return stream ? static_cast<hipStream_t>(stream) : c->stream;
 }
@@ -156,7 +173,7 @@ int derive_key_dev(Ctx *c, uint8_t out[32], const uint8_t salt[32],
   HIP_TRY(launch_keyed_hash(j, 0, c->stream));
   HIP_TRY(hipMemcpyAsync(c->h_small.p, d_out, 32, hipMemcpyDeviceToHost,
                          c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(stream_wait(c->stream));
   memcpy(out, c->h_small.p, 32);
   return 0;
 }
@@ -237,7 +254,7 @@ int build_up(Ctx *c, hipStream_t s, const Salts &salts, const uint8_t *cid_key,
         return e;
       *posts += 1;
       HIP_TRY(hipMemcpyAsync(root_ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
+      HIP_TRY(stream_wait(s));
       return 0;
     }
     const uint64_t m = (nodes + bf - 1) / bf;
@@ -396,7 +413,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
   if (int e = c->h_small.ensure(64)) return e;
   HIP_TRY(hipMemcpyAsync(c->h_small.p, c->d_refs.p, 64, hipMemcpyDeviceToHost,
                          c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(stream_wait(c->stream));
   memcpy(ref, c->h_small.p, 64);
   if (w->post) {
     int rc = w->post(w->post_ctx, kind, ref, w->h_one.p, n);
@@ -651,7 +668,7 @@ int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
   HIP_TRY(hipMemcpyAsync(ref_out, c->d_refs.p, 64, hipMemcpyDeviceToHost, c->stream));
   if (ctext_out && n)
     HIP_TRY(hipMemcpyAsync(ctext_out, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(stream_wait(c->stream));
   return 0;
 }
 
@@ -695,7 +712,7 @@ int glfsx_post_batch(const uint8_t salt[32], const void *ptext, uint64_t total,
     if (ctext_out)
       HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(ctext_out) + off, c->d_ct.p,
                              bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(stream_wait(c->stream));
   }
   return 0;
 }
@@ -893,7 +910,7 @@ int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
     cid_words(j, cid_key);
     HIP_TRY(launch_post(j, s));
     HIP_TRY(hipMemcpyAsync(out->ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(stream_wait(s));
     posts = 1;
   } else {
     const uint64_t n1 = (n0 + bf - 1) / bf;
@@ -960,7 +977,7 @@ int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
                          c->d_ct.u8(), RefLayout{c->d_refs.u8(), ~0ull, 0}))
     return e;
   HIP_TRY(hipMemcpyAsync(level1_out, c->d_refs.p, m * 64, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return 0;
 }
 
@@ -1011,7 +1028,7 @@ int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
   words_from_key(k, dek);
   HIP_TRY(launch_chacha_xor(k, c->d_in.u8(), c->d_ct.u8(), n, c->stream));
   HIP_TRY(hipMemcpyAsync(dst, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(stream_wait(c->stream));
   return 0;
 }
 
@@ -1091,7 +1108,7 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
   if (post && span)
     HIP_TRY(hipMemcpyAsync(h_ct.data(), c->d_ct.p, span, hipMemcpyDeviceToHost,
                            c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(stream_wait(c->stream));
   if (post) {
     for (uint64_t i = 0; i < n; ++i) {
       // one PostBlob per blob, in order: its single Post (a data block, or
