@@ -748,6 +748,183 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   }
 }
 
+// ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
+// A BLAKE3 chunk is 16 dependent compressions; in a launch that leaves one
+// wave per SIMD their latency is the pass's latency.  Here lane q of a quad
+// holds column q of the 4x4 state (a = v[q], b = v[4+q], c = v[8+q],
+// d = v[12+q]) and runs one G per step; the diagonal step rotates rows b, c,
+// d across the quad by DPP quad_perm and back.  The 16 message words sit in
+// the quad's 64-B LDS slot; lane q reads the four it needs per round (words
+// s_r[2q], s_r[2q+1], s_r[8+2q], s_r[9+2q]) at offsets fixed per lane.  A
+// chaining value ends up as cv[q] = a ^ c, cv[4+q] = b ^ d in lane q.
+// 1024-lane workgroups: 256 quads = 256 chunks (256 KiB) per workgroup; the
+// workgroup's subtree is merged pairwise through the slots (the same
+// left-complete tree as tree_reduce), and k_merge finishes split messages.
+__device__ __forceinline__ uint32_t qrot1(uint32_t x) {  // lane q <- lane q+1
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(x), 0x39, 0xF, 0xF, true));
+}
+__device__ __forceinline__ uint32_t qrot2(uint32_t x) {  // lane q <- lane q+2
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(x), 0x4E, 0xF, 0xF, true));
+}
+__device__ __forceinline__ uint32_t qrot3(uint32_t x) {  // lane q <- lane q+3
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(x), 0x93, 0xF, 0xF, true));
+}
+
+#define QG(a, b, c, d, x, y) \
+  a = a + b + (x);           \
+  d = rotr(d ^ a, 16);       \
+  c = c + d;                 \
+  b = rotr(b ^ c, 12);       \
+  a = a + b + (y);           \
+  d = rotr(d ^ a, 8);        \
+  c = c + d;                 \
+  b = rotr(b ^ c, 7);
+
+// One compression in quad layout.  addr[4r+k]: LDS byte address of the k-th
+// message word this lane uses in round r.  On return (a, b) = (cv[q], cv[4+q]).
+__device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
+                                              uint32_t c, uint32_t d,
+                                              const uint32_t (&addr)[28]) {
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const uint32_t m0 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r]);
+    const uint32_t m1 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 1]);
+    const uint32_t m2 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 2]);
+    const uint32_t m3 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 3]);
+    QG(a, b, c, d, m0, m1);
+    b = qrot1(b);
+    c = qrot2(c);
+    d = qrot3(d);
+    QG(a, b, c, d, m2, m3);
+    b = qrot3(b);
+    c = qrot2(c);
+    d = qrot1(d);
+  }
+  a ^= c;
+  b ^= d;
+}
+
+__device__ __forceinline__ uint32_t qsel(uint32_t q, uint32_t x0, uint32_t x1,
+                                         uint32_t x2, uint32_t x3) {
+  return q == 0 ? x0 : q == 1 ? x1 : q == 2 ? x2 : x3;
+}
+
+// The 28 LDS addresses of a 64-B slot at byte `slot` for lane q.
+__device__ __forceinline__ void quad_addrs(uint32_t (&addr)[28], uint32_t slot,
+                                           uint32_t q) {
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    constexpr int kk[4] = {0, 1, 8, 9};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w = qsel(q, kSched.s[r][kk[k]], kSched.s[r][kk[k] + 2],
+                              kSched.s[r][kk[k] + 4], kSched.s[r][kk[k] + 6]);
+      addr[4 * r + k] = slot + 4u * w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_quad(KArgs a) {
+  __shared__ uint4 slots[256 * 4];      // 64 B message slot per quad
+  __shared__ uint32_t passbuf[8];       // the odd subtree passing up a level
+  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
+  const uint64_t j = blockIdx.x >> a.split_log2;
+  const uint32_t sidx = blockIdx.x & ((1u << a.split_log2) - 1u);
+  const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
+  constexpr uint64_t kSpan = 256ull << 10;
+  const uint64_t c0b = uint64_t(sidx) * kSpan;
+  if (sidx != 0 && c0b >= len) return;  // empty sub-range (uniform)
+  const bool whole = len <= kSpan;       // the message fits this workgroup
+  const uint64_t mylen = min(len - c0b, kSpan);
+  const uint32_t cnt = mylen ? uint32_t((mylen + 1023) >> 10) : 1u;
+  const uint8_t *msg = a.src + j * a.stride + c0b;
+  const uint32_t slot = lds_offset(slots + quad * 4);
+  const uint32_t kq_lo = qsel(q, a.key[0], a.key[1], a.key[2], a.key[3]);
+  const uint32_t kq_hi = qsel(q, a.key[4], a.key[5], a.key[6], a.key[7]);
+  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+  uint32_t addr[28];
+  quad_addrs(addr, slot, q);
+  uint32_t cl = kq_lo, ch = kq_hi;  // this quad's chaining value
+  if (quad < cnt) {
+    const uint64_t coff = uint64_t(quad) << 10;
+    const uint32_t clen = uint32_t(min<uint64_t>(mylen - coff, 1024));
+    const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
+    const uint32_t ctr = sidx * 256u + quad;  // chunk counter (messages < 4 GiB)
+    const uint8_t *cp = msg + coff + 16u * q;
+    uint4 blk[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      blk[b] = make_uint4(0, 0, 0, 0);
+      const int32_t avail = int32_t(clen) - 64 * b - 16 * int32_t(q);
+      if (avail >= 16) {
+        blk[b] = *reinterpret_cast<const uint4 *>(cp + 64 * b);
+      } else if (avail > 0) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int i = 0; i < avail; ++i) w[i >> 2] |= uint32_t(cp[64 * b + i]) << (8 * (i & 3));
+        blk[b] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      if (uint32_t(b) < nb) {
+        *reinterpret_cast<lds_u32x4 *>(slot + 16u * q) =
+            u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
+        uint32_t fl = a.base;
+        if (b == 0) fl |= kChunkStart;
+        if (uint32_t(b) + 1 == nb) {
+          fl |= kChunkEnd;
+          if (whole && cnt == 1) fl |= kRoot;
+        }
+        const uint32_t dq = qsel(q, ctr, 0u, blen, fl);
+        quad_compress(cl, ch, ivq, dq, addr);
+        // the slot is rewritten next block: reads of this block are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+  }
+  // the workgroup's subtree: pairwise through the slots
+  uint32_t count = cnt;
+  while (count > 1) {  // uniform
+    const uint32_t half = count >> 1, odd = count & 1u;
+    __syncthreads();  // slots of the previous level have been read
+    if (quad < count) {
+      if (odd && quad == count - 1) {
+        passbuf[q] = cl;
+        passbuf[4 + q] = ch;
+      } else {
+        uint32_t *ps = reinterpret_cast<uint32_t *>(slots + (quad >> 1) * 4);
+        ps[(quad & 1u) * 8 + q] = cl;
+        ps[(quad & 1u) * 8 + 4 + q] = ch;
+      }
+    }
+    __syncthreads();
+    if (quad < half) {
+      const uint32_t fl = a.base | kParent | ((whole && count == 2) ? kRoot : 0u);
+      cl = kq_lo;
+      ch = kq_hi;
+      const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
+      quad_compress(cl, ch, ivq, dq, addr);
+    } else if (odd && quad == half) {
+      cl = passbuf[q];
+      ch = passbuf[4 + q];
+    }
+    count = half + odd;
+  }
+  if (quad == 0) {  // lanes 0-3: words q and 4+q of the result
+    uint32_t *dst;
+    if (whole) {
+      dst = reinterpret_cast<uint32_t *>(a.refs + (j / a.ref_bf) * a.ref_stride +
+                                         (j % a.ref_bf) * 64 + a.out_off);
+    } else {
+      dst = a.scratch + uint64_t(blockIdx.x) * 8;
+    }
+    dst[q] = cl;
+    dst[4 + q] = ch;
+  }
+}
+
 // Split mode, second phase: one 64-lane workgroup per message merges the
 // subtree CVs of its W = ceil(len / span) workgroups (W <= 64) and writes the
 // root output.  Messages that fit one workgroup were finished by k_pass.
@@ -1120,12 +1297,51 @@ void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   *sl_out = sl;
 }
 
+bool quad_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GLFSX_QUAD");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// BLAKE3-only pass in quad layout (k_quad): latency-bound launches of at
+// most 16384 chunks, messages of at most 64 x 256 KiB.
+hipError_t launch_quad(KArgs a, uint64_t maxlen, hipStream_t s) {
+  constexpr uint64_t kSpan = 256ull << 10;
+  const uint64_t W = maxlen > kSpan ? (maxlen + kSpan - 1) / kSpan : 1;
+  uint32_t sl = 0;
+  while ((1ull << sl) < W) ++sl;
+  a.split_log2 = sl;
+  a.scratch = nullptr;
+  if (sl) {
+    hipError_t e = scratch_get(&a.scratch, size_t(a.n << sl) * 32, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_quad, dim3(uint32_t(a.n << sl)), dim3(1024), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || sl == 0) return e;
+  hipLaunchKernelGGL(k_merge, dim3(uint32_t(a.n)), dim3(64), 0, s, a, kSpan);
+  return hipGetLastError();
+}
+
+bool quad_ok(const KArgs &a, uint64_t maxlen, bool aligned, uint32_t sl) {
+  const uint64_t chunks = a.n * (maxlen ? (maxlen + 1023) >> 10 : 1);
+  const bool refs4 = ((reinterpret_cast<uintptr_t>(a.refs) | a.out_off |
+                       a.ref_stride) & 3) == 0;
+  return quad_enabled() && aligned && refs4 && (a.n << sl) <= latency_wgs() &&
+         chunks <= 16384 && maxlen <= (64ull * 256) << 10;
+}
+
 template <bool CHACHA>
 hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
                        hipStream_t s) {
   int g;
   uint32_t sl;
   pass_plan(a.n, maxlen, &g, &sl);
+  if constexpr (!CHACHA) {
+    if (quad_ok(a, maxlen, aligned, sl)) return launch_quad(a, maxlen, s);
+  }
   a.split_log2 = sl;
   a.scratch = nullptr;
   if (sl) {
