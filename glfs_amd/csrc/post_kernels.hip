@@ -427,6 +427,121 @@ __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
   b3_compress<A>(cv, m, chunk, 0u, 64u, fl);
 }
 
+// GLFSX_PIPE: the pair's second keystream block is computed interleaved
+// with the first block's compression (two independent ARX streams in one
+// region instead of strict phases); same instructions, same results.
+#ifndef GLFSX_PIPE
+#define GLFSX_PIPE 1
+#endif
+#define CDR_A(x)                     \
+  CQR_A(x[0], x[4], x[8], x[12]);    \
+  CQR_A(x[1], x[5], x[9], x[13]);    \
+  CQR_A(x[2], x[6], x[10], x[14]);   \
+  CQR_A(x[3], x[7], x[11], x[15]);   \
+  CQR_A(x[0], x[5], x[10], x[15]);   \
+  CQR_A(x[1], x[6], x[11], x[12]);   \
+  CQR_A(x[2], x[7], x[8], x[13]);    \
+  CQR_A(x[3], x[4], x[9], x[14]);
+
+// one BLAKE3 G and one ChaCha20 quarter-round, step by step (the two
+// have the same add / xor-rotate shape): two independent chains per step
+#define GQ_A(a, b, c, d, mx, my, e, f, g, h)                  \
+  a = add3_a(a, b, (mx)); e = add_a(e, f);                    \
+  d = rotr_a<16>(xor_a(d, a)); h = rotr_a<16>(xor_a(h, e));   \
+  c = add_a(c, d); g = add_a(g, h);                           \
+  b = rotr_a<12>(xor_a(b, c)); f = rotr_a<20>(xor_a(f, g));   \
+  a = add3_a(a, b, (my)); e = add_a(e, f);                    \
+  d = rotr_a<8>(xor_a(d, a)); h = rotr_a<24>(xor_a(h, e));    \
+  c = add_a(c, d); g = add_a(g, h);                           \
+  b = rotr_a<7>(xor_a(b, c)); f = rotr_a<25>(xor_a(f, g));
+
+// BLAKE3 round R of v fused with one ChaCha20 double round of x
+template <int R>
+__device__ __forceinline__ void gq_round(uint32_t (&v)[16], const uint32_t (&m)[16],
+                                         uint32_t (&x)[16]) {
+  constexpr const int *s = kSched.s[R];
+  GQ_A(v[0], v[4], v[8], v[12], m[s[0]], m[s[1]], x[0], x[4], x[8], x[12]);
+  GQ_A(v[1], v[5], v[9], v[13], m[s[2]], m[s[3]], x[1], x[5], x[9], x[13]);
+  GQ_A(v[2], v[6], v[10], v[14], m[s[4]], m[s[5]], x[2], x[6], x[10], x[14]);
+  GQ_A(v[3], v[7], v[11], v[15], m[s[6]], m[s[7]], x[3], x[7], x[11], x[15]);
+  GQ_A(v[0], v[5], v[10], v[15], m[s[8]], m[s[9]], x[0], x[5], x[10], x[15]);
+  GQ_A(v[1], v[6], v[11], v[12], m[s[10]], m[s[11]], x[1], x[6], x[11], x[12]);
+  GQ_A(v[2], v[7], v[8], v[13], m[s[12]], m[s[13]], x[2], x[7], x[8], x[13]);
+  GQ_A(v[3], v[4], v[9], v[14], m[s[14]], m[s[15]], x[3], x[4], x[9], x[14]);
+}
+
+__device__ __forceinline__ void stage_half(uint32_t wa, uint32_t half,
+                                           const uint32_t (&m)[16]) {
+  wa = opaque(wa);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<lds_u32x4 *>(wa ^ ((4u * half + q) << 4)) =
+        u32x4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
+}
+
+// Both blocks of a pair in the LDS-staged CID pass (asm ARX form):
+// ChaCha(a); then BLAKE3(a) interleaved round by round with ChaCha(b);
+// then BLAKE3(b).
+__device__ __forceinline__ void pair_pipelined(
+    uint32_t (&cv)[8], const uint4 &a0, const uint4 &a1, const uint4 &a2,
+    const uint4 &a3, const uint4 &b0, const uint4 &b1, const uint4 &b2,
+    const uint4 &b3, uint32_t chunk, uint32_t blk, uint32_t fla, uint32_t flb,
+    const uint32_t (&dek)[8], uint32_t wa) {
+  constexpr uint32_t c0 = 0x61707865u, c1 = 0x3320646eu, c2 = 0x79622d32u,
+                     c3 = 0x6b206574u;
+  uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                    a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+  const uint32_t ctr_a = (chunk << 4) + blk;
+  {
+    uint32_t x[16];
+    chacha_block<true>(x, dek, ctr_a);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+  }
+  stage_half(wa, 0, m);
+  // block b's keystream state, round 1 in C (key-only quarter-rounds hoist)
+  const uint32_t ctr_b = ctr_a + 1;
+  uint32_t x[16] = {c0, c1, c2, c3, dek[0], dek[1], dek[2], dek[3],
+                    dek[4], dek[5], dek[6], dek[7], ctr_b, 0u, 0u, 0u};
+  CQR(x[0], x[4], x[8], x[12]);
+  CQR(x[1], x[5], x[9], x[13]);
+  CQR(x[2], x[6], x[10], x[14]);
+  CQR(x[3], x[7], x[11], x[15]);
+  CQR(x[0], x[5], x[10], x[15]);
+  CQR(x[1], x[6], x[11], x[12]);
+  CQR(x[2], x[7], x[8], x[13]);
+  CQR(x[3], x[4], x[9], x[14]);
+  // BLAKE3(a): round 0 alone (C form, IV literals), rounds 1-6 step by
+  // step with ChaCha(b)'s double rounds 2-7, then ChaCha(b)'s last three
+  uint32_t v[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
+                    kIV[0], kIV[1], kIV[2], kIV[3], chunk, 0u, 64u, fla};
+  b3_round<0, true>(v, m);
+  gq_round<1>(v, m, x);
+  gq_round<2>(v, m, x);
+  gq_round<3>(v, m, x);
+  gq_round<4>(v, m, x);
+  gq_round<5>(v, m, x);
+  gq_round<6>(v, m, x);
+  CDR_A(x);
+  CDR_A(x);
+  CDR_A(x);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
+  x[0] += c0;
+  x[1] += c1;
+  x[2] += c2;
+  x[3] += c3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[4 + i] += dek[i];
+  x[12] += ctr_b;
+  uint32_t mb[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
+                     b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mb[i] ^= x[i];
+  stage_half(wa, 1, mb);
+  b3_compress<true>(cv, mb, chunk, 0u, 64u, flb);
+}
+
 // Fast path: the lane's G chunks are all full (16*G consecutive 64-B blocks,
 // 16-B aligned).  Blocks go in pairs through two named register buffers: the
 // odd block's loads are issued before the even block is compressed and the
@@ -520,6 +635,12 @@ __device__ __forceinline__ void lane_subtree_full(
         b3 = nb[3];
       }
       constexpr bool stg = CHACHA && STAGE;
+      if constexpr (GLFSX_PIPE && gl && stg && A) {
+        uint32_t fb = base;
+        if (pp == 7) fb |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
+        pair_pipelined(cv, a0, a1, a2, a3, b0, b1, b2, b3, chunk, 2 * pp,
+                       base | (pp == 0 ? kChunkStart : 0u), fb, dek, wst);
+      } else {
       full_block<CHACHA, stg, A>(cv, a0, a1, a2, a3, chunk, 2 * pp,
                          base | (pp == 0 ? kChunkStart : 0u), dek,
                          cq && !stg ? cq + 4 * blk : nullptr, wst, 0);
@@ -534,6 +655,7 @@ __device__ __forceinline__ void lane_subtree_full(
       if (pp == 7) fl |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
       full_block<CHACHA, stg, A>(cv, b0, b1, b2, b3, chunk, 2 * pp + 1, fl, dek,
                          cq && !stg ? cq + 4 * (blk + 1) : nullptr, wst, 1);
+      }
       if (stg) {
         // lane l stores piece pc of line 8k + r: each store instruction
         // writes 8 whole 128-B lines.  Line 8k+r's slot for pc is
