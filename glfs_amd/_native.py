@@ -71,6 +71,9 @@ SIGNATURES = {
     "glfsx_writer_new": (_VP, [_U64, _U64, _CP, _CP, POST_FN, _VP,
                                ctypes.POINTER(ctypes.c_int)]),
     "glfsx_writer_write": (_INT, [_VP, _VP, _SZ]),
+    "glfsx_writer_flush": (_INT, [_VP]),
+    "glfsx_writer_set_strict": (_INT, [_VP, _INT]),
+    "glfsx_writer_error": (_CP, [_VP]),
     "glfsx_writer_finish": (_INT, [_VP, ctypes.POINTER(glfsx_root)]),
     "glfsx_writer_free": (None, [_VP]),
     "glfsx_create": (_INT, [_U64, _U64, _CP, _CP, _VP, _U64, POST_FN, _VP,
@@ -121,10 +124,11 @@ def last_error() -> str:
     return (lib.glfsx_last_error() or b"").decode(errors="replace")
 
 
-def check(rc: int) -> None:
+def check(rc: int, msg: str | None = None) -> None:
     if rc == GLFSX_OK:
         return
-    msg = last_error()
+    if msg is None:
+        msg = last_error()
     if rc in (GLFSX_E_BLOCKSIZE_GT_MAX, GLFSX_E_BLOCKSIZE_LT_MIN):
         raise Panic(rc, msg)
     if rc == GLFSX_E_STORE:

@@ -114,7 +114,7 @@ class Writer:
     """blob.go:71-83 Writer (NewWriter/Write/Finish)."""
 
     def __init__(self, machine: "Machine", store: WO, salt: Optional[bytes],
-                 cid_key: Optional[bytes] = None):
+                 cid_key: Optional[bytes] = None, strict: bool = False):
         self._cb, self._errors = _make_post_cb(store)
         err = ctypes.c_int(0)
         self._w = N.lib.glfsx_writer_new(machine.block_size, store.max_size(),
@@ -122,11 +122,21 @@ class Writer:
                                          ctypes.byref(err))
         if not self._w:
             N.check(err.value)
+        if strict:
+            # blob.go:120-133 error timing: every Write returns after the
+            # Posts of the blocks it completed were delivered
+            N.check(N.lib.glfsx_writer_set_strict(self._w, 1))
 
     def _raise(self, rc: int):
         if rc == N.GLFSX_E_STORE and self._errors:
             raise StoreError(rc, repr(self._errors[0])) from self._errors[0]
-        N.check(rc)
+        N.check(rc, (N.lib.glfsx_writer_error(self._w) or b"").decode(errors="replace"))
+
+    def flush(self) -> None:
+        """Deliver the Posts of every complete block written so far."""
+        rc = N.lib.glfsx_writer_flush(self._w)
+        if rc:
+            self._raise(rc)
 
     def write(self, data: bytes) -> int:
         """blob.go:120-133."""
@@ -294,9 +304,9 @@ class Machine:
         return Ref.from_bytes(ref.raw)
 
     def new_writer(self, store: WO, salt: Optional[bytes] = None,
-                   cid_key: Optional[bytes] = None) -> Writer:
-        """blob.go:85-114."""
-        return Writer(self, store, salt, cid_key)
+                   cid_key: Optional[bytes] = None, strict: bool = False) -> Writer:
+        """blob.go:85-114 (strict: the reference's per-Write error timing)."""
+        return Writer(self, store, salt, cid_key, strict)
 
     def concat(self, store, block_size: int, salt: Optional[bytes], *roots: Root) -> Root:
         """blob.go:333-345."""

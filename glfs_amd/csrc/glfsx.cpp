@@ -13,6 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <mutex>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -119,16 +122,31 @@ int ctx_get(Ctx **out) {
 // for up to kSpinNs first: a blocking hipStreamSynchronize wakes the thread
 // tens of microseconds after the GPU finishes, which is most of the host
 // overhead of a short call (a 1 GiB Create takes ~1.3 ms); longer waits block.
+// At most kMaxSpinners threads poll at once (glfs.Machine is used
+// concurrently; N pollers would pin N host cores); the rest block at once,
+// and a poller yields its core between queries.
 constexpr int64_t kSpinNs = 2000000;
+constexpr int kMaxSpinners = 2;
+std::atomic<int> g_spinners{0};
 hipError_t stream_wait(hipStream_t s) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t e = hipStreamQuery(s);
-    if (e != hipErrorNotReady) return e;
-    if (std::chrono::duration_cast<std::chrono::nanoseconds>(
-            std::chrono::steady_clock::now() - t0).count() > kSpinNs)
-      return hipStreamSynchronize(s);
+  if (g_spinners.fetch_add(1, std::memory_order_relaxed) >= kMaxSpinners) {
+    g_spinners.fetch_sub(1, std::memory_order_relaxed);
+    return hipStreamSynchronize(s);
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e;
+  for (;;) {
+    e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) break;
+    if (std::chrono::duration_cast<std::chrono::nanoseconds>(
+            std::chrono::steady_clock::now() - t0).count() > kSpinNs) {
+      e = hipStreamSynchronize(s);
+      break;
+    }
+    sched_yield();
+  }
+  g_spinners.fetch_sub(1, std::memory_order_relaxed);
+  return e;
 }
 
 hipStream_t pick_stream(Ctx *c, void *stream) {
@@ -194,29 +212,35 @@ struct Salts {
 };
 
 // blob.go:99-101.  DeriveKey is a pure function, so the (salt -> indexSalt,
-// rawSalt) pairs are memoised per thread: NewWriter is called once per blob by
-// glfs.PostBlob (machine.go:64) and would otherwise cost two launches each.
+// rawSalt) pairs are memoised (process-wide): NewWriter is called once per
+// blob by glfs.PostBlob (machine.go:64) and would otherwise cost two launches
+// each.
 struct SaltCacheEntry {
   uint8_t salt[32];
   Salts s;
 };
-thread_local std::vector<SaltCacheEntry> tls_salts;
+std::mutex g_salts_mu;
+std::vector<SaltCacheEntry> g_salts;
 
 int derive_salts(Ctx *c, const uint8_t *salt, Salts *s) {
   static const uint8_t zero[32] = {0};
   const uint8_t *sl = salt ? salt : zero;
-  for (const auto &e : tls_salts)
-    if (memcmp(e.salt, sl, 32) == 0) {
-      *s = e.s;
-      return 0;
-    }
+  {
+    std::lock_guard<std::mutex> lk(g_salts_mu);
+    for (const auto &e : g_salts)
+      if (memcmp(e.salt, sl, 32) == 0) {
+        *s = e.s;
+        return 0;
+      }
+  }
   if (int e = derive_key_dev(c, s->index, sl, "index", 5)) return e;
   if (int e = derive_key_dev(c, s->raw, sl, "raw", 3)) return e;
-  if (tls_salts.size() >= 64) tls_salts.erase(tls_salts.begin());
   SaltCacheEntry ent;
   memcpy(ent.salt, sl, 32);
   ent.s = *s;
-  tls_salts.push_back(ent);
+  std::lock_guard<std::mutex> lk(g_salts_mu);
+  if (g_salts.size() >= 64) g_salts.erase(g_salts.begin());
+  g_salts.push_back(ent);
   return 0;
 }
 
@@ -294,13 +318,23 @@ struct WSlot {
 
 // Staging slots outlive writers: glfs.PostBlob opens a Writer per blob
 // (machine.go:64), and pinned/device allocation costs far more than hashing a
-// small blob.  Freed writers return their slots here (per thread, bounded).
-thread_local std::vector<WSlot> tls_slot_pool;
+// small blob.  Freed writers return their slots and streams here.  The pools
+// are process-wide (keyed by device), so a writer may be created, used and
+// freed on different threads (a goroutine migrating between OS threads).
+// Staging of single synchronous posts (index nodes, a writer's tail block).
+struct OneBuf {
+  DevBuf d_in, d_ct, d_ref;
+  PinBuf h_ct, h_ref;
+  int dev = -1;
+};
+std::mutex g_pool_mu;
+std::vector<WSlot> g_slot_pool;
+std::vector<OneBuf> g_one_pool;
 struct StreamTriple {
   int dev;
   hipStream_t up, hash, down;
 };
-thread_local std::vector<StreamTriple> tls_stream_pool;
+std::vector<StreamTriple> g_stream_pool;
 
 void release_slot(WSlot &sl) {
   if (sl.h_in.p) (void)hipHostFree(sl.h_in.p);
@@ -318,10 +352,15 @@ void release_slot(WSlot &sl) {
 // GLFSX_SLOTS (2..4) and GLFSX_BATCH_MIB override the defaults (tuning).
 constexpr int kMaxSlots = 4;
 
+// A writer owns everything it touches after creation (streams, batch slots,
+// single-post staging, its device id and its last error text), so it does
+// not depend on the thread that created it: bigblob.Writer is
+// single-goroutine (blob.go:71-83), but a goroutine may run on any OS thread
+// between cgo calls.
 struct glfsx_writer {
-  Ctx *c = nullptr;
-  // batch streams (post_one uses the thread's): uploads, kernels, downloads,
-  // so batch k+1's H2D overlaps batch k's D2H on the full-duplex link
+  int dev = 0;
+  // batch streams: uploads, kernels (also the single posts), downloads, so
+  // batch k+1's H2D overlaps batch k's D2H on the full-duplex link
   hipStream_t ws = nullptr, s_up = nullptr, s_down = nullptr;
   uint64_t bs = 0, bf = 0;
   Salts salts{};
@@ -332,7 +371,7 @@ struct glfsx_writer {
   std::vector<std::vector<uint8_t>> indexes;  // index.go Index per level
   std::vector<uint64_t> counts;
   uint64_t size = 0;
-  PinBuf h_one;  // ctext of single posts (index nodes, the tail block)
+  OneBuf one;                // single posts (index nodes, the tail block)
   WSlot slot[kMaxSlots];
   int nslots = 3;
   int cur = 0;               // slot being filled
@@ -340,7 +379,10 @@ struct glfsx_writer {
   uint64_t batch_blocks = 1;
   uint64_t full = 0;         // complete blocks staged in slot[cur]
   uint64_t partial = 0;      // bytes of the block being filled
+  bool strict = false;       // deliver every completed block's Post before
+                             // Write returns (blob.go:120-133 error timing)
   int sticky = 0;            // first error; the writer is dead afterwards
+  std::string err;           // text of the last failed call on this writer
 };
 
 namespace {
@@ -386,37 +428,35 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
 }
 
 // Post one message from host memory (ref.go:98 post + sink), synchronously,
-// on the thread's stream.
+// on the writer's hash stream with the writer's own staging.
 int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
              const uint8_t *data, uint64_t n, uint8_t ref[64]) {
-  Ctx *c = w->c;
-  if (int e = c->d_in.ensure(n + 64)) return e;
-  if (int e = c->d_ct.ensure(n + 64)) return e;
-  if (int e = c->d_refs.ensure(64)) return e;
-  if (int e = w->h_one.ensure(n + 64)) return e;
+  OneBuf &o = w->one;
+  if (int e = o.d_in.ensure(n + 64)) return e;
+  if (int e = o.d_ct.ensure(n + 64)) return e;
+  if (int e = o.d_ref.ensure(64)) return e;
+  if (int e = o.h_ct.ensure(n + 64)) return e;
+  if (int e = o.h_ref.ensure(64)) return e;
   if (n)
-    HIP_TRY(hipMemcpyAsync(c->d_in.p, data, n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(o.d_in.p, data, n, hipMemcpyHostToDevice, w->ws));
   PostJob j{};
-  j.src = c->d_in.u8();
-  j.ctext = c->d_ct.u8();
+  j.src = o.d_in.u8();
+  j.ctext = o.d_ct.u8();
   j.stride = 0;
   j.msg_len = n;
   j.last_len = n;
   j.n = 1;
-  j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
+  j.out = RefLayout{o.d_ref.u8(), ~0ull, 0};
   words_from_key(j.salt, salt);
   cid_words(j, cidk(w));
-  HIP_TRY(launch_post(j, c->stream));
+  HIP_TRY(launch_post(j, w->ws));
   if (n)
-    HIP_TRY(hipMemcpyAsync(w->h_one.p, c->d_ct.p, n, hipMemcpyDeviceToHost,
-                           c->stream));
-  if (int e = c->h_small.ensure(64)) return e;
-  HIP_TRY(hipMemcpyAsync(c->h_small.p, c->d_refs.p, 64, hipMemcpyDeviceToHost,
-                         c->stream));
-  HIP_TRY(stream_wait(c->stream));
-  memcpy(ref, c->h_small.p, 64);
+    HIP_TRY(hipMemcpyAsync(o.h_ct.p, o.d_ct.p, n, hipMemcpyDeviceToHost, w->ws));
+  HIP_TRY(hipMemcpyAsync(o.h_ref.p, o.d_ref.p, 64, hipMemcpyDeviceToHost, w->ws));
+  HIP_TRY(stream_wait(w->ws));
+  memcpy(ref, o.h_ref.p, 64);
   if (w->post) {
-    int rc = w->post(w->post_ctx, kind, ref, w->h_one.p, n);
+    int rc = w->post(w->post_ctx, kind, ref, o.h_ct.p, n);
     if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
   }
   return 0;
@@ -739,7 +779,7 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
     return nullptr;
   }
   auto *w = new glfsx_writer();
-  w->c = c;
+  w->dev = c->dev;
   w->bs = bs;
   w->bf = bs / 64;  // blob.go:107
   if (int e = derive_salts(c, salt, &w->salts)) {
@@ -759,30 +799,41 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   if (const char *e = getenv("GLFSX_BATCH_MIB")) batch_mib = std::max(1ull, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GLFSX_SLOTS")) w->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
   w->batch_blocks = std::max<uint64_t>(1, (batch_mib << 20) / bs);
-  for (int k = 0; k < w->nslots; ++k) {
-    for (size_t i = tls_slot_pool.size(); i-- > 0;) {
-      if (tls_slot_pool[i].dev == c->dev) {
-        w->slot[k] = tls_slot_pool[i];
-        tls_slot_pool.erase(tls_slot_pool.begin() + i);
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (int k = 0; k < w->nslots; ++k) {
+      for (size_t i = g_slot_pool.size(); i-- > 0;) {
+        if (g_slot_pool[i].dev == w->dev) {
+          w->slot[k] = g_slot_pool[i];
+          g_slot_pool.erase(g_slot_pool.begin() + i);
+          break;
+        }
+      }
+      w->slot[k].dev = w->dev;
+    }
+    for (size_t i = g_one_pool.size(); i-- > 0;) {
+      if (g_one_pool[i].dev == w->dev) {
+        w->one = g_one_pool[i];
+        g_one_pool.erase(g_one_pool.begin() + i);
         break;
       }
     }
-    w->slot[k].dev = c->dev;
-  }
-  for (size_t i = tls_stream_pool.size(); i-- > 0;) {
-    if (tls_stream_pool[i].dev == c->dev) {
-      w->s_up = tls_stream_pool[i].up;
-      w->ws = tls_stream_pool[i].hash;
-      w->s_down = tls_stream_pool[i].down;
-      tls_stream_pool.erase(tls_stream_pool.begin() + i);
-      break;
+    w->one.dev = w->dev;
+    for (size_t i = g_stream_pool.size(); i-- > 0;) {
+      if (g_stream_pool[i].dev == w->dev) {
+        w->s_up = g_stream_pool[i].up;
+        w->ws = g_stream_pool[i].hash;
+        w->s_down = g_stream_pool[i].down;
+        g_stream_pool.erase(g_stream_pool.begin() + i);
+        break;
+      }
     }
   }
   if (!w->ws &&
       (hipStreamCreateWithFlags(&w->ws, hipStreamNonBlocking) != hipSuccess ||
        hipStreamCreateWithFlags(&w->s_up, hipStreamNonBlocking) != hipSuccess ||
        hipStreamCreateWithFlags(&w->s_down, hipStreamNonBlocking) != hipSuccess)) {
-    delete w;
+    glfsx_writer_free(w);
     *err = fail(GLFSX_E_DEVICE, "hipStreamCreate failed");
     return nullptr;
   }
@@ -790,51 +841,92 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   return w;
 }
 
+namespace {
+// Every writer entry point runs on the writer's device (the calling thread
+// may have another one current) and keeps the error text on the writer.
+struct WriterCall {
+  glfsx_writer *w;
+  explicit WriterCall(glfsx_writer *w_) : w(w_) { (void)hipSetDevice(w->dev); }
+  int done(int rc) {
+    if (rc) w->err = tls_err;
+    return rc;
+  }
+};
+
+// Drain: submit the staged complete blocks and deliver the Posts of every
+// batch in flight, oldest first.
+int drain(glfsx_writer *w) {
+  if (int e = submit(w)) return e;
+  for (;;) {
+    WSlot *o = nullptr;
+    for (auto &sl : w->slot)
+      if (sl.busy && (!o || sl.seq < o->seq)) o = &sl;
+    if (!o) return 0;
+    if (int e = complete(w, *o)) return e;
+  }
+}
+}  // namespace
+
 // blob.go:120-133: a block is complete exactly when buffered + incoming
 // reaches bs; complete blocks are hashed a batch at a time.
 int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
   if (!w) return fail(GLFSX_E_ARG, "null writer");
-  if (w->sticky) return w->sticky;
-  if (n && !data) return fail(GLFSX_E_ARG, "null data");
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (n && !data) return call.done(fail(GLFSX_E_ARG, "null data"));
   const uint8_t *p = static_cast<const uint8_t *>(data);
   while (n) {
     WSlot &sl = w->slot[w->cur];
     const uint64_t used = w->full * w->bs + w->partial;
     const uint64_t cap = w->batch_blocks * w->bs;  // slot holds up to a batch
     const uint64_t take = std::min<uint64_t>(cap - used, n);
-    if (int e = pin_grow(sl.h_in, used + take, used)) return w->sticky = e;
+    if (int e = pin_grow(sl.h_in, used + take, used)) return call.done(w->sticky = e);
     par_memcpy(sl.h_in.u8() + used, p, take);
     p += take;
     n -= take;
     w->full = (used + take) / w->bs;
     w->partial = (used + take) % w->bs;
     if (w->full == w->batch_blocks)
-      if (int e = submit(w)) return w->sticky = e;
+      if (int e = submit(w)) return call.done(w->sticky = e);
   }
+  if (w->strict)
+    if (int e = drain(w)) return call.done(w->sticky = e);
   return 0;
+}
+
+int glfsx_writer_flush(glfsx_writer *w) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (int e = drain(w)) return call.done(w->sticky = e);
+  return 0;
+}
+
+int glfsx_writer_set_strict(glfsx_writer *w, int strict) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  w->strict = strict != 0;
+  return 0;
+}
+
+const char *glfsx_writer_error(const glfsx_writer *w) {
+  return w ? w->err.c_str() : "null writer";
 }
 
 int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   if (!w || !out) return fail(GLFSX_E_ARG, "null argument");
-  if (w->sticky) return w->sticky;
-  if (int e = submit(w)) return w->sticky = e;
-  for (;;) {  // drain the batches still in flight, oldest first
-    WSlot *o = nullptr;
-    for (auto &sl : w->slot)
-      if (sl.busy && (!o || sl.seq < o->seq)) o = &sl;
-    if (!o) break;
-    if (int e = complete(w, *o)) return w->sticky = e;
-  }
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (int e = drain(w)) return call.done(w->sticky = e);
   if (w->partial) {  // blob.go:136-140: the tail block, never padded
     uint8_t ref[64];
     if (int e = post_one(w, 0, w->salts.raw, w->slot[w->cur].h_in.u8(), w->partial, ref))
-      return w->sticky = e;
-    if (int e = add_ref(w, 0, ref)) return w->sticky = e;
+      return call.done(w->sticky = e);
+    if (int e = add_ref(w, 0, ref)) return call.done(w->sticky = e);
     w->size += w->partial;
     w->partial = 0;
   }
   uint8_t root[64];
-  if (int e = finish_indexes(w, root)) return w->sticky = e;
+  if (int e = finish_indexes(w, root)) return call.done(w->sticky = e);
   memcpy(out->ref, root, 64);
   out->size = w->size;
   out->block_size = w->bs;
@@ -843,26 +935,39 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
 
 void glfsx_writer_free(glfsx_writer *w) {
   if (!w) return;
+  (void)hipSetDevice(w->dev);
   for (hipStream_t st : {w->s_up, w->ws, w->s_down})
     if (st) (void)hipStreamSynchronize(st);
-  for (auto &sl : w->slot) {
-    sl.busy = false;
-    sl.nblk = 0;
-    if (sl.dev >= 0 && tls_slot_pool.size() < 2 * kMaxSlots)
-      tls_slot_pool.push_back(sl);  // buffers are reused by the next writer
+  std::vector<hipStream_t> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto &sl : w->slot) {
+      sl.busy = false;
+      sl.nblk = 0;
+      if (sl.dev >= 0 && g_slot_pool.size() < 16 * kMaxSlots)
+        g_slot_pool.push_back(sl);  // buffers are reused by the next writer
+      else
+        release_slot(sl);
+    }
+    if (g_one_pool.size() < 16) {
+      g_one_pool.push_back(w->one);
+    } else {
+      OneBuf &o = w->one;
+      for (void *p : {o.d_in.p, o.d_ct.p, o.d_ref.p})
+        if (p) (void)hipFree(p);
+      for (void *p : {o.h_ct.p, o.h_ref.p})
+        if (p) (void)hipHostFree(p);
+    }
+    if (w->ws && g_stream_pool.size() < 16)
+      g_stream_pool.push_back({w->dev, w->s_up, w->ws, w->s_down});
     else
-      release_slot(sl);
+      drop = {w->s_up, w->ws, w->s_down};
   }
-  if (w->h_one.p) (void)hipHostFree(w->h_one.p);
-  if (w->ws && tls_stream_pool.size() < 4) {
-    tls_stream_pool.push_back({w->c->dev, w->s_up, w->ws, w->s_down});
-  } else {
-    for (hipStream_t st : {w->s_up, w->ws, w->s_down})
-      if (st) {
-        release_stream_scratch(st);
-        (void)hipStreamDestroy(st);
-      }
-  }
+  for (hipStream_t st : drop)
+    if (st) {
+      release_stream_scratch(st);
+      (void)hipStreamDestroy(st);
+    }
   delete w;
 }
 

@@ -31,9 +31,9 @@ struct PostJob {
   bool cid_keyed;
 };
 
-// Largest message the workgroup-per-message kernels accept (256 lanes x 64
-// BLAKE3 chunks).
-constexpr uint64_t kMaxMsgLen = 256ull * 64 * 1024;
+// Largest message (bigblob block or index node) the post kernels accept:
+// 256 workgroups x 256 lanes x 64 BLAKE3 chunks (split mode, 4 GiB).
+constexpr uint64_t kMaxMsgLen = 256ull * 256 * 64 * 1024;
 
 hipError_t launch_post(const PostJob &job, hipStream_t s);
 

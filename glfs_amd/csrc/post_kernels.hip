@@ -328,11 +328,31 @@ struct KArgs {
   uint32_t out_off;  // byte offset of the 32-byte result inside the ref slot
   // split mode (few messages): 2^split_log2 workgroups per message, each over
   // 256*G consecutive chunks; their subtree CVs go to scratch (8 words per
-  // workgroup) and k_merge finishes the tree.  split_log2 == 0: one
-  // workgroup per message, no scratch.
+  // workgroup) and the message's last-arriving workgroup (per-message
+  // arrival counter in cnt, zero between launches) finishes the tree.
+  // split_log2 == 0: one workgroup per message, no scratch.
   uint32_t split_log2;
   uint32_t *scratch;
+  uint32_t *cnt;
 };
+
+// Split mode: publish this workgroup's subtree CV (thread 0 stored it to
+// scratch) and count it in; true in every thread of the workgroup that
+// arrives last for its message, which then merges all W CVs.  Agent-scope
+// release / acquire: the workgroups of one message run on different XCDs,
+// whose L2s are not coherent with each other without them.
+__device__ __forceinline__ bool arrive_last(uint32_t *cnt, uint32_t W,
+                                            uint32_t t, uint32_t *flag) {
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old + 1 == W;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return last;
+}
 
 // Merge step after the last block of local chunk jj: pop/parent/push on the
 // lane's CV stack (eager merges = ctz(jj+1); final merges empty the stack).
@@ -635,7 +655,9 @@ __device__ __forceinline__ void lane_subtree_full(
         b3 = nb[3];
       }
       constexpr bool stg = CHACHA && STAGE;
-      if constexpr (GLFSX_PIPE && gl && stg && A) {
+      // (the other branch is the same template as the latency-mode C-form
+      // pass, which tests/test_gpu_parity.py::test_arx_forms_vs_oracle runs)
+      if constexpr (GLFSX_PIPE && GLFSX_ASM_ARX == 1 && gl && stg && A) {
         uint32_t fb = base;
         if (pp == 7) fb |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
         pair_pipelined(cv, a0, a1, a2, a3, b0, b1, b2, b3, chunk, 2 * pp,
@@ -859,14 +881,35 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   }
   __syncthreads();
   tree_reduce(lds, active, t, key, a.base, !split, cv);
+  if (!split) {
+    if (t == 0) store_digest(ref + a.out_off, cv);
+    return;
+  }
+  // split (uniform): this workgroup's subtree CV to scratch; the message's
+  // last workgroup merges the W = ceil(len / span) CVs (left-complete tree,
+  // ROOT on the last parent) and resets the counter for the next launch
+  const uint64_t wbase = j << a.split_log2;
   if (t == 0) {
-    if (split) {  // this workgroup's subtree CV, finished by k_merge
-      uint4 *q = reinterpret_cast<uint4 *>(a.scratch + uint64_t(blockIdx.x) * 8);
-      q[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
-      q[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
-    } else {
-      store_digest(ref + a.out_off, cv);
-    }
+    uint4 *q = reinterpret_cast<uint4 *>(a.scratch + (wbase + sidx) * 8);
+    q[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+    q[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+  }
+  const uint32_t W = uint32_t((len_full + kSpan - 1) / kSpan);
+  __shared__ uint32_t s_flag;
+  if (!arrive_last(a.cnt + j, W, t, &s_flag)) return;
+  if (t < W) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(a.scratch + (wbase + t) * 8);
+    const uint4 x = q[0], y = q[1];
+    cv[0] = x.x; cv[1] = x.y; cv[2] = x.z; cv[3] = x.w;
+    cv[4] = y.x; cv[5] = y.y; cv[6] = y.z; cv[7] = y.w;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
+  }
+  __syncthreads();
+  tree_reduce(lds, W, t, key, a.base, true, cv);
+  if (t == 0) {
+    store_digest(ref + a.out_off, cv);
+    a.cnt[j] = 0;
   }
 }
 
@@ -881,7 +924,8 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
 // chaining value ends up as cv[q] = a ^ c, cv[4+q] = b ^ d in lane q.
 // 1024-lane workgroups: 256 quads = 256 chunks (256 KiB) per workgroup; the
 // workgroup's subtree is merged pairwise through the slots (the same
-// left-complete tree as tree_reduce), and k_merge finishes split messages.
+// left-complete tree as tree_reduce), and the last workgroup of a split
+// message merges the workgroups' CVs.
 __device__ __forceinline__ uint32_t qrot1(uint32_t x) {  // lane q <- lane q+1
   return uint32_t(__builtin_amdgcn_mov_dpp(int(x), 0x39, 0xF, 0xF, true));
 }
@@ -1034,46 +1078,70 @@ __global__ __launch_bounds__(1024) void k_quad(KArgs a) {
     }
     count = half + odd;
   }
-  if (quad == 0) {  // lanes 0-3: words q and 4+q of the result
-    uint32_t *dst;
-    if (whole) {
-      dst = reinterpret_cast<uint32_t *>(a.refs + (j / a.ref_bf) * a.ref_stride +
-                                         (j % a.ref_bf) * 64 + a.out_off);
-    } else {
-      dst = a.scratch + uint64_t(blockIdx.x) * 8;
+  uint32_t *const out = reinterpret_cast<uint32_t *>(
+      a.refs + (j / a.ref_bf) * a.ref_stride + (j % a.ref_bf) * 64 + a.out_off);
+  if (whole) {
+    if (quad == 0) {  // lanes 0-3: words q and 4+q of the result
+      out[q] = cl;
+      out[4 + q] = ch;
     }
-    dst[q] = cl;
-    dst[4 + q] = ch;
+    return;
   }
-}
-
-// Split mode, second phase: one 64-lane workgroup per message merges the
-// subtree CVs of its W = ceil(len / span) workgroups (W <= 64) and writes the
-// root output.  Messages that fit one workgroup were finished by k_pass.
-__global__ __launch_bounds__(64) void k_merge(KArgs a, uint64_t span) {
-  __shared__ uint32_t lds[64 * 8];
-  const uint64_t j = blockIdx.x;
-  const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
-  if (len <= span) return;
-  const uint32_t W = uint32_t((len + span - 1) / span);
-  const uint32_t t = threadIdx.x;
-  uint32_t key[8], p[8];
+  // split: subtree CV to scratch; the message's last workgroup merges the W
+  // CVs through the slots exactly like its own subtree (ROOT at the top)
+  const uint64_t wbase = j << a.split_log2;
+  if (tid < 64) {  // wave 0: quad 0's CV into lane 0, which stores it and
+                   // then releases it (arrive_last) in program order
+    uint32_t w[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = a.key[i];
-  if (t < W) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(
-        a.scratch + ((j << a.split_log2) + t) * 8);
-    const uint4 x = q[0], y = q[1];
-    p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
-    p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) lds[t * 8 + i] = p[i];
+    for (int k = 0; k < 4; ++k) {
+      w[k] = __builtin_amdgcn_readlane(cl, k);
+      w[4 + k] = __builtin_amdgcn_readlane(ch, k);
+    }
+    if (tid == 0) {
+      uint4 *p = reinterpret_cast<uint4 *>(a.scratch + (wbase + sidx) * 8);
+      p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
   }
-  __syncthreads();
-  tree_reduce(lds, W, t, key, a.base, true, p);
-  if (t == 0) {
-    uint8_t *ref = a.refs + (j / a.ref_bf) * a.ref_stride + (j % a.ref_bf) * 64;
-    store_digest(ref + a.out_off, p);
+  const uint32_t W = uint32_t((len + kSpan - 1) / kSpan);
+  __shared__ uint32_t s_flag;
+  if (!arrive_last(a.cnt + j, W, tid, &s_flag)) return;
+  if (quad < W) {
+    cl = a.scratch[(wbase + quad) * 8 + q];
+    ch = a.scratch[(wbase + quad) * 8 + 4 + q];
+  }
+  count = W;
+  while (count > 1) {  // uniform
+    const uint32_t half = count >> 1, odd = count & 1u;
+    __syncthreads();
+    if (quad < count) {
+      if (odd && quad == count - 1) {
+        passbuf[q] = cl;
+        passbuf[4 + q] = ch;
+      } else {
+        uint32_t *ps = reinterpret_cast<uint32_t *>(slots + (quad >> 1) * 4);
+        ps[(quad & 1u) * 8 + q] = cl;
+        ps[(quad & 1u) * 8 + 4 + q] = ch;
+      }
+    }
+    __syncthreads();
+    if (quad < half) {
+      const uint32_t fl = a.base | kParent | (count == 2 ? kRoot : 0u);
+      cl = kq_lo;
+      ch = kq_hi;
+      const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
+      quad_compress(cl, ch, ivq, dq, addr);
+    } else if (odd && quad == half) {
+      cl = passbuf[q];
+      ch = passbuf[4 + q];
+    }
+    count = half + odd;
+  }
+  if (quad == 0) {
+    out[q] = cl;
+    out[4 + q] = ch;
+    if (q == 0) a.cnt[j] = 0;
   }
 }
 
@@ -1334,10 +1402,6 @@ hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
     hipLaunchKernelGGL((k_pass<G, CHACHA, true>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL((k_pass<G, CHACHA, false>), grid, block, 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.split_log2 == 0) return e;
-  hipLaunchKernelGGL(k_merge, dim3(uint32_t(a.n)), dim3(64), 0, s, a,
-                     uint64_t(256 * G) << 10);
   return hipGetLastError();
 }
 
@@ -1349,55 +1413,69 @@ uint32_t split_target_default() {
   return e ? uint32_t(strtoul(e, nullptr, 10)) : 2048u;
 }
 std::atomic<uint32_t> g_split_target{split_target_default()};
-constexpr uint32_t kMaxSplitLog2 = 6;  // k_merge merges <= 64 subtrees
+constexpr uint32_t kMaxSplitLog2 = 8;  // the last workgroup merges <= 256 CVs
 
-// Split-mode scratch (32 B per workgroup): one persistent buffer per
-// (device, stream), reused by every launch on that stream -- launches on one
-// stream are ordered, so the buffer is never shared by two in flight.  The
-// stream-ordered pool (hipMallocAsync / hipFreeAsync per launch) serialised
-// the Writer's three-stream pipeline (host round trip 43.5 -> 24 GiB/s).
-// A buffer only grows when the split target is raised at run time; the old
-// one is released after its stream drains.
+// Split-mode scratch (32 B per workgroup) and arrival counters (4 B per
+// message, zero between launches: each message's last workgroup resets its
+// own): one persistent pair of buffers per (device, stream), reused by every
+// launch on that stream -- launches on one stream are ordered, so they are
+// never shared by two in flight.  The stream-ordered pool (hipMallocAsync /
+// hipFreeAsync per launch) serialised the Writer's three-stream pipeline
+// (host round trip 43.5 -> 24 GiB/s).  A buffer only grows when a launch
+// needs more; the old one is released after its stream drains.
 struct ScratchSlot {
   int dev;
   hipStream_t stream;
   uint32_t *p;
   size_t bytes;
+  uint32_t *cnt;
+  size_t cnt_words;
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
 
-hipError_t scratch_get(uint32_t **p, size_t bytes, hipStream_t s) {
-  std::mutex &mu = g_scratch_mu;
-  std::vector<ScratchSlot> &slots = g_scratch;
+hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
+  const size_t bytes = size_t(wgs) * 32, words = size_t(msgs);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lk(mu);
-  for (ScratchSlot &sl : slots) {
-    if (sl.dev != dev || sl.stream != s) continue;
-    if (sl.bytes >= bytes) {
-      *p = sl.p;
-      return hipSuccess;
-    }
-    e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return e;
-    (void)hipFree(sl.p);
-    sl.p = nullptr;
-    sl.bytes = 0;
-    e = hipMalloc(reinterpret_cast<void **>(&sl.p), bytes);
-    if (e != hipSuccess) return e;
-    sl.bytes = bytes;
-    *p = sl.p;
-    return hipSuccess;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  ScratchSlot *sl = nullptr;
+  for (ScratchSlot &x : g_scratch)
+    if (x.dev == dev && x.stream == s) sl = &x;
+  if (!sl) {
+    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0});
+    sl = &g_scratch.back();
   }
-  // at least the default target's worst case, so it never needs to grow
-  const size_t want = bytes > (size_t(2) << 16) ? bytes : (size_t(2) << 16);
-  uint32_t *q = nullptr;
-  e = hipMalloc(reinterpret_cast<void **>(&q), want);
-  if (e != hipSuccess) return e;
-  slots.push_back({dev, s, q, want});
-  *p = q;
+  if (sl->bytes < bytes || sl->cnt_words < words) {
+    if (sl->p || sl->cnt) {
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return e;
+    }
+    if (sl->bytes < bytes) {
+      if (sl->p) (void)hipFree(sl->p);
+      sl->p = nullptr;
+      sl->bytes = 0;
+      // at least the default target's worst case, so it rarely grows
+      const size_t want = std::max(bytes, size_t(2) << 16);
+      e = hipMalloc(reinterpret_cast<void **>(&sl->p), want);
+      if (e != hipSuccess) return e;
+      sl->bytes = want;
+    }
+    if (sl->cnt_words < words) {
+      if (sl->cnt) (void)hipFree(sl->cnt);
+      sl->cnt = nullptr;
+      sl->cnt_words = 0;
+      const size_t want = std::max(words, size_t(4096));
+      e = hipMalloc(reinterpret_cast<void **>(&sl->cnt), want * 4);
+      if (e != hipSuccess) return e;
+      e = hipMemsetAsync(sl->cnt, 0, want * 4, s);
+      if (e != hipSuccess) return e;
+      sl->cnt_words = want;
+    }
+  }
+  a->scratch = sl->p;
+  a->cnt = sl->cnt;
   return hipSuccess;
 }
 
@@ -1406,10 +1484,13 @@ hipError_t scratch_get(uint32_t **p, size_t bytes, hipStream_t s) {
 void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   const uint64_t C = maxlen ? (maxlen + 1023) >> 10 : 1;
   int g = 1;
-  while (256ull * g < C) g *= 2;
+  while (256ull * g < C && g < 64) g *= 2;
+  // messages above 256 lanes x 64 chunks (16 MiB) always span several
+  // workgroups
+  uint32_t sl = 0;
+  while ((256ull * g << sl) < C) ++sl;
   // few messages: halve the chunks per lane and double the workgroups per
   // message until the launch fills the chip (256 CUs x 8 workgroups)
-  uint32_t sl = 0;
   const uint64_t target = g_split_target.load(std::memory_order_relaxed);
   while (g > 1 && sl < kMaxSplitLog2 && (n << sl) < target) {
     g /= 2;
@@ -1436,14 +1517,12 @@ hipError_t launch_quad(KArgs a, uint64_t maxlen, hipStream_t s) {
   while ((1ull << sl) < W) ++sl;
   a.split_log2 = sl;
   a.scratch = nullptr;
+  a.cnt = nullptr;
   if (sl) {
-    hipError_t e = scratch_get(&a.scratch, size_t(a.n << sl) * 32, s);
+    hipError_t e = scratch_get(&a, a.n << sl, a.n, s);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_quad, dim3(uint32_t(a.n << sl)), dim3(1024), 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || sl == 0) return e;
-  hipLaunchKernelGGL(k_merge, dim3(uint32_t(a.n)), dim3(64), 0, s, a, kSpan);
   return hipGetLastError();
 }
 
@@ -1466,8 +1545,9 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
   }
   a.split_log2 = sl;
   a.scratch = nullptr;
+  a.cnt = nullptr;
   if (sl) {
-    hipError_t e = scratch_get(&a.scratch, size_t(a.n << sl) * 32, s);
+    hipError_t e = scratch_get(&a, a.n << sl, a.n, s);
     if (e != hipSuccess) return e;
   }
   hipError_t e;
@@ -1549,10 +1629,12 @@ void release_stream_scratch(hipStream_t s) {
   for (size_t i = 0; i < g_scratch.size(); ++i) {
     if (g_scratch[i].stream != s) continue;
     int cur = 0;
-    if (hipGetDevice(&cur) == hipSuccess && cur == g_scratch[i].dev)
-      (void)hipFree(g_scratch[i].p);
-    else
+    if (hipGetDevice(&cur) == hipSuccess && cur == g_scratch[i].dev) {
+      if (g_scratch[i].p) (void)hipFree(g_scratch[i].p);
+      if (g_scratch[i].cnt) (void)hipFree(g_scratch[i].cnt);
+    } else {
       continue;  // another device's stream of the same handle value
+    }
     g_scratch[i] = g_scratch.back();
     g_scratch.pop_back();
     --i;

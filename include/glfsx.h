@@ -34,8 +34,14 @@
  *     binding re-panics; store failures come back as GLFSX_E_STORE with the
  *     sink's code in glfsx_last_error().
  *   - The caller owns every buffer; nothing is retained after return (cgo rule).
- *   - Reentrant: each host thread gets its own HIP stream and staging buffers;
- *     glfsx_set_device() selects the GPU for the calling thread.
+ *   - Reentrant: each host thread gets its own HIP stream and staging buffers
+ *     for the one-shot calls; glfsx_set_device() selects the GPU for the
+ *     calling thread.  A writer owns its streams, staging, device and error
+ *     text, so consecutive calls on one writer may come from different
+ *     threads (a goroutine migrating between OS threads); one call at a time.
+ *   - glfsx_last_error() is thread-local: read it in the same C call that
+ *     failed (a cgo binding does so in its C preamble), or use
+ *     glfsx_writer_error() for writer calls.
  *   - Ref layout (ref.go:77-82): 64 bytes = CID[32] || DEK[32].
  */
 #ifndef GLFSX_H
@@ -144,9 +150,21 @@ typedef struct glfsx_writer glfsx_writer;
 glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
                                const uint8_t *salt, const uint8_t *cid_key,
                                glfsx_post_fn post, void *post_ctx, int *err);
-/* blob.go:120-133.  Data blocks are hashed in batches: a store error is
- * returned by the Write or Finish call whose batch contained the failure. */
+/* blob.go:120-133.  Data blocks are hashed in pipelined batches: by default
+ * a store error is returned by the Write or Finish call whose batch contained
+ * the failure (Posts are still delivered in the reference's order, and none
+ * after the failing one).  In strict mode (glfsx_writer_set_strict) every
+ * Write returns only after the Posts of all blocks it completed were
+ * delivered, so the error comes from the Write that filled the failing block,
+ * exactly as blob.go:120-133 returns it. */
 int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n);
+/* Deliver the Posts of every complete block written so far (no reference
+ * counterpart: the reference never holds a complete block back). */
+int glfsx_writer_flush(glfsx_writer *w);
+/* strict != 0: blob.go:120-133 error timing (see glfsx_writer_write). */
+int glfsx_writer_set_strict(glfsx_writer *w, int strict);
+/* Text of the last failed call on this writer (any thread). */
+const char *glfsx_writer_error(const glfsx_writer *w);
 /* blob.go:135-150 */
 int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out);
 void glfsx_writer_free(glfsx_writer *w);
