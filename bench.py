@@ -198,6 +198,7 @@ def main():
             if world == 1:   # the CPU baseline is an N=1 figure (rank 0 only)
                 out["cpu_baseline"] = cpu_baseline(args)
             out["small_blobs"] = small_blobs(torch, N, stream, sp)
+            out["config4_end_to_end"] = config4_end_to_end(torch, N, stream, sp)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -352,6 +353,123 @@ def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=5):
             "blobs_per_s": round(n / (ms * 1e-3)), "ms": round(ms, 3),
             "what": "1,048,576 distinct 4 KiB blobs, glfs.PostBlob roots (DEK + ChaCha20 "
                     "ctext to HBM + CID), one lane per blob"}
+
+
+def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
+    """BASELINE config 4 end to end: 1,048,576 distinct 4 KiB blobs (blob i =
+    splitmix stream of seed i) posted as glfs blobs (DEK + ChaCha20 ctext to
+    HBM + CID per blob, machine.go:64), then the tree of them ("%07d" names,
+    tree.go:250-260 PostTreeMap): its JSON lines encoded and the tree blob
+    posted through the bigblob write path (2 MiB blocks + index node).
+    Two routes, both timed from blobs resident in HBM to the tree root:
+      device: roots stay in HBM, lines encoded on the GPU
+              (glfsx_tree_encode_device), tree blob = glfsx_create_device;
+      host:   roots copied to the host, lines encoded on host cores
+              (glfsx_tree_encode, C++), tree blob through the Writer from
+              host memory (glfsx_create, H2D + D2H of its ctext, counting
+              sink).
+    The per-entry ExistsUnit store lookup (tree.go:304) is the store's and
+    is not in either route (the blobs were just posted).  value = blob bytes
+    / time."""
+    import numpy as np
+    from glfs_amd import glfs
+    bs = 2 << 20
+    m = glfs.Machine()
+    blob_salt, tree_salt = m.make_salt("blob"), m.make_salt("tree")
+    cuda = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    names_h = np.frombuffer("".join("%07d" % i for i in range(n)).encode(), dtype=np.uint8)
+    name_offs_h = np.arange(n + 1, dtype=np.uint64) * 7
+    types_h = np.frombuffer(b"blob" * n, dtype=np.uint8)
+    type_offs_h = np.arange(n + 1, dtype=np.uint64) * 4
+    modes_h = np.full(n, 0o644, dtype=np.uint32)
+    sizes_h = np.full(n, ln, dtype=np.uint64)
+    bss_h = np.full(n, bs, dtype=np.uint64)
+    with torch.cuda.stream(stream):
+        data = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
+        ct = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
+        roots = torch.empty(64 * n, dtype=torch.uint8, device="cuda")
+        offs = torch.arange(n, dtype=torch.int64, device="cuda") * ln
+        lens = torch.full((n,), ln, dtype=torch.int64, device="cuda")
+        names = cuda(names_h)
+        name_offs = cuda(name_offs_h.view(np.int64))
+        types = cuda(types_h)
+        type_offs = cuda(type_offs_h.view(np.int64))
+        modes = cuda(modes_h.view(np.int32))
+        bss = cuda(bss_h.view(np.int64))
+        lines = torch.empty(260 * n, dtype=torch.uint8, device="cuda")
+        tree_ct = torch.empty(260 * n, dtype=torch.uint8, device="cuda")
+        N.check(N.lib.glfsx_fill_splitmix_blobs_device(data.data_ptr(), n, ln, 0, sp))
+    stream.synchronize()
+    roots_h = torch.empty(64 * n, dtype=torch.uint8).pin_memory()
+    lines_h = np.empty(260 * n, dtype=np.uint8)
+    total = ctypes.c_uint64()
+    root = N.glfsx_root()
+    counts = (ctypes.c_uint64 * 2)()
+    sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
+
+    def post_blobs():
+        N.check(N.lib.glfsx_post_blobs_device(bs, blob_salt, None, data.data_ptr(),
+                                              offs.data_ptr(), lens.data_ptr(), n, ln,
+                                              ct.data_ptr(), roots.data_ptr(), sp))
+
+    def device_route():
+        post_blobs()
+        N.check(N.lib.glfsx_tree_encode_device(n, names.data_ptr(), name_offs.data_ptr(),
+                                               modes.data_ptr(), types.data_ptr(),
+                                               type_offs.data_ptr(), roots.data_ptr(),
+                                               lens.data_ptr(), bss.data_ptr(),
+                                               lines.data_ptr(), lines.numel(), None,
+                                               ctypes.byref(total), sp))
+        N.check(N.lib.glfsx_create_device(bs, tree_salt, None, lines.data_ptr(), total.value,
+                                          tree_ct.data_ptr(), ctypes.byref(root), None, sp))
+        return bytes(root.ref)
+
+    def host_route():
+        post_blobs()
+        with torch.cuda.stream(stream):
+            roots_h.copy_(roots, non_blocking=True)
+        stream.synchronize()
+        N.check(N.lib.glfsx_tree_encode(n, names_h.ctypes.data, name_offs_h.ctypes.data,
+                                        modes_h.ctypes.data, types_h.ctypes.data,
+                                        type_offs_h.ctypes.data, roots_h.data_ptr(),
+                                        sizes_h.ctypes.data, bss_h.ctypes.data,
+                                        lines_h.ctypes.data, lines_h.size,
+                                        ctypes.byref(total), None))
+        counts[0] = counts[1] = 0
+        N.check(N.lib.glfsx_create(bs, bs, tree_salt, None, lines_h.ctypes.data, total.value,
+                                   sink, ctypes.byref(counts), ctypes.byref(root)))
+        return bytes(root.ref)
+
+    res = {}
+    for name, fn in (("device", device_route), ("host", host_route)):
+        fn()
+        ts = []
+        for _ in range(reps):
+            stream.synchronize()
+            t = time.perf_counter()
+            r = fn()
+            stream.synchronize()
+            ts.append(time.perf_counter() - t)
+        sec = min(ts)
+        res[name] = {"value": round(n * ln / GIB / sec, 2), "unit": "GiB/s",
+                     "ms": round(sec * 1e3, 3), "blobs_per_s": round(n / sec),
+                     "tree_bytes": total.value, "tree_root_cid": r[:32].hex()}
+    # the device route's pieces (HIP events on the launch stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    post_blobs()
+    ev[1].record(stream)
+    ev[1].synchronize()
+    res["device"]["post_blobs_ms"] = round(ev[0].elapsed_time(ev[1]), 3)
+    assert res["device"]["tree_root_cid"] == res["host"]["tree_root_cid"]
+    out = dict(res["device"])
+    out["what"] = ("1,048,576 x 4 KiB glfs blobs (HBM) -> roots -> PostTreeMap JSON lines "
+                   "(\"%07d\" names) -> tree blob root; lines encoded on the GPU, tree "
+                   "posted from HBM; value = blob bytes / time")
+    out["host_encode_route"] = res["host"]
+    out["host_encode_route"]["what"] = ("same, roots D2H, lines on host cores "
+                                        "(glfsx_tree_encode), tree via the Writer from host")
+    return out
 
 
 def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):

@@ -93,6 +93,11 @@ SIGNATURES = {
     "glfsx_fill_splitmix_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
     "glfsx_decrypt_batch_device": (_INT, [_VP, _U64, _U64, _VP, _VP, _VP]),
     "glfsx_sink_count": (_INT, [_VP, _INT, _VP, _VP, _U64]),
+    "glfsx_tree_encode": (_INT, [_U64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _U64,
+                                 ctypes.POINTER(ctypes.c_uint64), _VP]),
+    "glfsx_tree_encode_device": (_INT, [_U64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
+                                        _U64, _VP, ctypes.POINTER(ctypes.c_uint64), _VP]),
+    "glfsx_fill_splitmix_blobs_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
     "glfsx_depth": (_INT, [_U64, _U64]),
     "glfsx_branching_factor": (_U64, [_U64]),
 }

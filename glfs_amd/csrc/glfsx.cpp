@@ -85,7 +85,7 @@ struct PinBuf {
 struct Ctx {
   int dev = -1;
   hipStream_t stream = nullptr;
-  DevBuf d_in, d_ct, d_refs, d_lvl_a, d_lvl_b, d_small;
+  DevBuf d_in, d_ct, d_refs, d_lvl_a, d_lvl_b, d_small, d_tree;
   PinBuf h_small;
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
@@ -1146,14 +1146,9 @@ int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
   if (!d_data || !d_offsets || !d_lengths || !d_roots)
     return fail(GLFSX_E_ARG, "null argument");
   if (int e = check_block_size(block_size)) return e;
-  if (max_len > block_size)
-    return fail(GLFSX_E_ARG, "blob of %llu bytes spans more than one %llu-byte block",
-                (unsigned long long)max_len, (unsigned long long)block_size);
-  if (max_len > kMaxSmallLen)
-    return fail(GLFSX_E_UNSUPPORTED, "small-blob kernel limited to %llu bytes",
-                (unsigned long long)kMaxSmallLen);
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
+  hipStream_t s = pick_stream(c, stream);
   Salts salts;
   if (int e = derive_salts(c, salt, &salts)) return e;
   SmallJob j{};
@@ -1172,9 +1167,65 @@ int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
   } else {
     blake3_iv_words(j.cid_key);
   }
-  HIP_TRY(launch_post_small(j, pick_stream(c, stream)));
+  // blobs of <= 16 KiB: one lane each (k_small skips the others)
+  HIP_TRY(launch_post_small(j, s));
+  if (max_len <= kMaxSmallLen) return 0;
+  // larger blobs (the caller said some may exceed 16 KiB): find them, then
+  // one post each (<= one block: the root is post(rawSalt, blob),
+  // blob.go:190-193) or a whole Create (several blocks)
+  std::vector<uint64_t> offs(n), lens(n);
+  HIP_TRY(hipMemcpyAsync(offs.data(), d_offsets, 8 * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(lens.data(), d_lengths, 8 * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(stream_wait(s));
+  for (uint64_t i = 0; i < n; ++i) {
+    if (lens[i] <= kMaxSmallLen) continue;
+    const uint8_t *src = static_cast<const uint8_t *>(d_data) + offs[i];
+    uint8_t *ct = d_ctext ? static_cast<uint8_t *>(d_ctext) + offs[i] : nullptr;
+    uint8_t *ref = static_cast<uint8_t *>(d_roots) + 64 * i;
+    if (lens[i] <= block_size) {
+      PostJob pj{};
+      pj.src = src;
+      pj.ctext = ct;
+      pj.stride = 0;
+      pj.msg_len = lens[i];
+      pj.last_len = lens[i];
+      pj.n = 1;
+      pj.out = RefLayout{ref, ~0ull, 0};
+      words_from_key(pj.salt, salts.raw);
+      cid_words(pj, cid_key);
+      HIP_TRY(launch_post(pj, s));
+    } else {
+      glfsx_root r;
+      if (int e = glfsx_create_device(block_size, salt, cid_key, src, lens[i], ct, &r,
+                                      nullptr, s))
+        return e;
+      HIP_TRY(hipMemcpyAsync(ref, r.ref, 64, hipMemcpyHostToDevice, s));
+      HIP_TRY(stream_wait(s));  // r lives on this frame
+    }
+  }
   return 0;
 }
+
+namespace {
+// A store sink that keeps every Post (large blobs of glfsx_post_blobs are
+// created first and their Posts replayed in call order).
+struct CapturedPost {
+  int kind;
+  uint8_t ref[64];
+  std::vector<uint8_t> ctext;
+};
+int capture_post(void *ctx, int kind, const uint8_t *ref, const void *ctext,
+                 uint64_t len) {
+  auto *v = static_cast<std::vector<CapturedPost> *>(ctx);
+  v->emplace_back();
+  CapturedPost &p = v->back();
+  p.kind = kind;
+  memcpy(p.ref, ref, 64);
+  p.ctext.assign(static_cast<const uint8_t *>(ctext),
+                 static_cast<const uint8_t *>(ctext) + len);
+  return 0;
+}
+}  // namespace
 
 int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
                      const uint8_t *cid_key, const void *data,
@@ -1188,39 +1239,70 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
     return fail(GLFSX_E_BLOCKSIZE_GT_MAX, "blockSize %llu > maxSize %llu",
                 (unsigned long long)bs, (unsigned long long)store_max);
   if (int e = check_block_size(bs)) return e;
-  uint64_t span = 0, max_len = 0;
+  // small blobs go through the device batch; larger ones (any size) are
+  // Created one by one through the Writer, their Posts captured
+  std::vector<uint64_t> soffs(n), slens(n);
+  std::vector<std::vector<CapturedPost>> big(n);
+  uint64_t span = 0, max_len = 0, n_small = 0;
   for (uint64_t i = 0; i < n; ++i) {
-    span = std::max(span, offsets[i] + lengths[i]);
-    max_len = std::max(max_len, lengths[i]);
+    const bool small = lengths[i] <= kMaxSmallLen;
+    soffs[i] = offsets[i];
+    slens[i] = small ? lengths[i] : kMaxSmallLen + 1;  // skipped by k_small
+    if (small) {
+      ++n_small;
+      span = std::max(span, offsets[i] + lengths[i]);
+      max_len = std::max(max_len, lengths[i]);
+    } else {
+      glfsx_root r;
+      if (int e = glfsx_create(bs, store_max, salt, cid_key,
+                               static_cast<const uint8_t *>(data) + offsets[i],
+                               lengths[i], capture_post, &big[i], &r))
+        return e;
+      memcpy(roots_out + 64 * i, r.ref, 64);
+    }
   }
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
-  if (int e = c->d_in.ensure(span + 64)) return e;
-  if (int e = c->d_ct.ensure(span + 64)) return e;
-  if (int e = c->d_refs.ensure(64 * n)) return e;
-  if (int e = c->d_lvl_a.ensure(16 * n)) return e;
   std::vector<uint8_t> h_ct(post ? span + 1 : 0);
-  uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_lvl_a.p);
-  uint64_t *d_len = d_off + n;
-  HIP_TRY(hipMemcpyAsync(c->d_in.p, data, span, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_off, offsets, 8 * n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_len, lengths, 8 * n, hipMemcpyHostToDevice, c->stream));
-  if (int e = glfsx_post_blobs_device(bs, salt, cid_key, c->d_in.p, d_off, d_len, n,
-                                      max_len, c->d_ct.p, c->d_refs.p, c->stream))
-    return e;
-  HIP_TRY(hipMemcpyAsync(roots_out, c->d_refs.p, 64 * n, hipMemcpyDeviceToHost,
-                         c->stream));
-  if (post && span)
-    HIP_TRY(hipMemcpyAsync(h_ct.data(), c->d_ct.p, span, hipMemcpyDeviceToHost,
+  if (n_small) {
+    if (int e = c->d_in.ensure(span + 64)) return e;
+    if (int e = c->d_ct.ensure(span + 64)) return e;
+    if (int e = c->d_refs.ensure(64 * n)) return e;
+    if (int e = c->d_lvl_a.ensure(16 * n)) return e;
+    uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_lvl_a.p);
+    uint64_t *d_len = d_off + n;
+    if (span)
+      HIP_TRY(hipMemcpyAsync(c->d_in.p, data, span, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_off, soffs.data(), 8 * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_len, slens.data(), 8 * n, hipMemcpyHostToDevice, c->stream));
+    if (int e = glfsx_post_blobs_device(bs, salt, cid_key, c->d_in.p, d_off, d_len, n,
+                                        max_len, c->d_ct.p, c->d_refs.p, c->stream))
+      return e;
+    std::vector<uint8_t> refs(64 * n);
+    HIP_TRY(hipMemcpyAsync(refs.data(), c->d_refs.p, 64 * n, hipMemcpyDeviceToHost,
                            c->stream));
-  HIP_TRY(stream_wait(c->stream));
+    if (post && span)
+      HIP_TRY(hipMemcpyAsync(h_ct.data(), c->d_ct.p, span, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIP_TRY(stream_wait(c->stream));
+    for (uint64_t i = 0; i < n; ++i)
+      if (lengths[i] <= kMaxSmallLen) memcpy(roots_out + 64 * i, &refs[64 * i], 64);
+  }
   if (post) {
     for (uint64_t i = 0; i < n; ++i) {
-      // one PostBlob per blob, in order: its single Post (a data block, or
-      // the empty index node, blob.go:187-189)
-      int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
-                    h_ct.data() + offsets[i], lengths[i]);
-      if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+      // one PostBlob per blob, in order: a small blob's single Post (a data
+      // block, or the empty index node, blob.go:187-189), or a large blob's
+      // whole Post sequence
+      if (lengths[i] <= kMaxSmallLen) {
+        int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
+                      h_ct.data() + offsets[i], lengths[i]);
+        if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+      } else {
+        for (const CapturedPost &p : big[i]) {
+          int rc = post(post_ctx, p.kind, p.ref, p.ctext.data(), p.ctext.size());
+          if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+        }
+      }
     }
   }
   return 0;
@@ -1251,6 +1333,62 @@ int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
                          static_cast<uint8_t *>(d_ptext), n, block_size,
                          total - (n - 1) * block_size,
                          static_cast<const uint8_t *>(d_refs), pick_stream(c, stream)));
+  return 0;
+}
+
+int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,
+                             const uint64_t *d_name_offs, const uint32_t *d_modes,
+                             const uint8_t *d_types, const uint64_t *d_type_offs,
+                             const uint8_t *d_roots, const uint64_t *d_sizes,
+                             const uint64_t *d_block_sizes, void *d_out,
+                             uint64_t out_cap, uint64_t *d_line_ends,
+                             uint64_t *out_len, void *stream) {
+  if (!out_len) return fail(GLFSX_E_ARG, "null out_len");
+  *out_len = 0;
+  if (n == 0) return 0;
+  if (!d_name_offs || !d_modes || !d_type_offs || !d_roots || !d_sizes ||
+      !d_block_sizes)
+    return fail(GLFSX_E_ARG, "null argument");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  hipStream_t s = pick_stream(c, stream);
+  const uint64_t words = n + (n + 255) / 256 + 1;
+  if (int e = c->d_tree.ensure(8 * words)) return e;
+  if (int e = c->h_small.ensure(64)) return e;
+  TreeJob j{};
+  j.n = n;
+  j.names = d_names;
+  j.name_offs = d_name_offs;
+  j.modes = d_modes;
+  j.types = d_types;
+  j.type_offs = d_type_offs;
+  j.roots = d_roots;
+  j.sizes = d_sizes;
+  j.block_sizes = d_block_sizes;
+  j.scratch = reinterpret_cast<uint64_t *>(c->d_tree.p);
+  j.total = j.scratch + words - 1;
+  j.line_ends = d_line_ends;
+  j.out = static_cast<uint8_t *>(d_out);
+  j.cap = d_out ? out_cap : 0;
+  HIP_TRY(launch_tree_encode(j, s));
+  HIP_TRY(hipMemcpyAsync(c->h_small.p, j.total, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(stream_wait(s));
+  memcpy(out_len, c->h_small.p, 8);
+  if (d_out && *out_len > out_cap)
+    return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
+                (unsigned long long)*out_len, (unsigned long long)out_cap);
+  return 0;
+}
+
+int glfsx_fill_splitmix_blobs_device(void *d_dst, uint64_t n, uint64_t len,
+                                     uint64_t seed0, void *stream) {
+  if (n && len && !d_dst) return fail(GLFSX_E_ARG, "null argument");
+  if (len % 8 || (reinterpret_cast<uintptr_t>(d_dst) & 7))
+    return fail(GLFSX_E_ARG, "blob length and pointer must be multiples of 8");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  HIP_TRY(launch_fill_blobs(static_cast<uint8_t *>(d_dst), n, len, seed0,
+                            pick_stream(c, stream)));
   return 0;
 }
 

@@ -51,8 +51,9 @@ hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
                              uint8_t *dst, uint64_t n, hipStream_t s);
 
 // Many small blobs, one lane each (glfs.PostBlob batched): blob i is
-// src[offs[i] .. offs[i]+lens[i]), 0 <= lens[i] <= kMaxSmallLen; its root ref
-// (CID || DEK) goes to refs + 64*i.  Empty blobs use index_salt.
+// src[offs[i] .. offs[i]+lens[i]); if lens[i] <= kMaxSmallLen its root ref
+// (CID || DEK) goes to refs + 64*i (empty blobs use index_salt); longer blobs
+// are skipped (the caller posts them).
 constexpr uint64_t kMaxSmallLen = 16ull * 1024;
 struct SmallJob {
   const uint8_t *src;
@@ -85,6 +86,29 @@ uint32_t set_latency_wgs(uint32_t wgs);
 // Drop the split-mode scratch kept for stream s (call before destroying s,
 // after it has drained).
 void release_stream_scratch(hipStream_t s);
+
+// Tree JSON lines on the device (tree_kernels.hip): see glfsx_tree_encode.
+struct TreeJob {
+  uint64_t n;
+  const uint8_t *names;
+  const uint64_t *name_offs;  // n + 1
+  const uint32_t *modes;
+  const uint8_t *types;
+  const uint64_t *type_offs;  // n + 1
+  const uint8_t *roots;       // 64 B per entry
+  const uint64_t *sizes, *block_sizes;
+  uint64_t *scratch;          // n + ceil(n / 256) words
+  uint64_t *line_ends;        // nullable
+  uint64_t *total;            // device word: total bytes
+  uint8_t *out;               // nullable: lengths only
+  uint64_t cap;               // bytes at out
+};
+hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
+
+// n blobs of len bytes (len % 8 == 0), blob b = the splitmix stream of seed
+// seed0 + b (see oracle_fill_splitmix_blobs).
+hipError_t launch_fill_blobs(uint8_t *dst, uint64_t n, uint64_t len, uint64_t seed0,
+                             hipStream_t s);
 
 void words_from_key(uint32_t w[8], const uint8_t key[32]);
 void blake3_iv_words(uint32_t w[8]);

@@ -21,6 +21,7 @@
 // Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
 #include "kernels.h"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -1170,6 +1171,7 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
   const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
   if (i >= a.n) return;  // no barriers in this kernel
   const uint64_t off = a.offs[i], len = a.lens[i];
+  if (len > kMaxSmallLen) return;  // posted by the host's large-blob route
   const uint8_t *msg = a.src + off;
   uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + off : nullptr;
   uint8_t *ref = a.refs + i * 64;
@@ -1714,7 +1716,8 @@ hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
 
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   if (job.n == 0) return hipSuccess;
-  if (job.max_len > kMaxSmallLen) return hipErrorInvalidValue;
+  // blobs above kMaxSmallLen are skipped by k_small (posted elsewhere)
+  const uint64_t max_len = std::min(job.max_len, kMaxSmallLen);
   SArgs a{};
   a.src = job.src;
   a.ctext = job.ctext;
@@ -1728,12 +1731,12 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   }
   a.base = kKeyed;
   a.out_off = 32;
-  hipError_t e = launch_small_pass<false>(a, job.max_len, s);
+  hipError_t e = launch_small_pass<false>(a, max_len, s);
   if (e != hipSuccess) return e;
   for (int i = 0; i < 8; ++i) a.key[i] = a.key0[i] = job.cid_key[i];
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;
-  return launch_small_pass<true>(a, job.max_len, s);
+  return launch_small_pass<true>(a, max_len, s);
 }
 
 hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,

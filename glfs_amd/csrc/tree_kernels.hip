@@ -1,0 +1,310 @@
+// tree_kernels.hip -- gfx950 kernels for the glfs tree path (BASELINE config
+// 4) and per-blob synthetic inputs.
+//
+// k_tree_len / k_tree_prefix / k_tree_write: TreeWriter.Put's JSON lines
+// (tree.go:300-316, json.Encoder.Encode(TreeEntry)) for n entries whose refs
+// are already in HBM (the roots glfsx_post_blobs_device wrote), so a tree of
+// a million blobs is encoded and hashed without leaving the device.  Same
+// bytes as the host encoder (tree.cpp) and glfs_amd/tree.py's
+// entry_json_line: encoding/json's appendString with escapeHTML, decimal
+// numbers, the cid as a hex string (parity unpinned at that one field, see
+// tree.cpp).
+//
+// Layout: one thread per entry.  k_tree_len computes each line's length and
+// a 256-entry workgroup-inclusive scan; k_tree_prefix scans the workgroup
+// totals (one workgroup); k_tree_write builds the workgroup's 256 lines in
+// LDS at the alignment of their destination and stores them with aligned
+// 16-byte stores (bytes at the two partial 16-byte granules of a
+// workgroup's span, which it shares with its neighbours, are stored one by
+// one).  A workgroup whose lines do not fit the LDS image stores bytes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace glfsx {
+namespace {
+
+struct TArgs {
+  uint64_t n;
+  const uint8_t *names;
+  const uint64_t *name_offs;
+  const uint32_t *modes;
+  const uint8_t *types;
+  const uint64_t *type_offs;
+  const uint8_t *roots;
+  const uint64_t *sizes, *block_sizes;
+  uint64_t *local_end;  // per entry: inclusive end within its workgroup
+  uint64_t *wg_total;   // per workgroup: total bytes, then (k_tree_prefix)
+                        // the exclusive prefix
+  uint64_t *line_ends;  // nullable: global inclusive line ends
+  uint8_t *out;
+  uint64_t cap;         // bytes at out; nothing is written if the total exceeds it
+  const uint64_t *total;
+};
+
+constexpr uint32_t kImg = 60 * 1024;  // LDS image per workgroup
+
+__device__ const char kHexD[] = "0123456789abcdef";
+
+// Go's utf8.DecodeRune (see tree.cpp)
+__device__ __forceinline__ void decode_rune(const uint8_t *p, uint64_t n,
+                                            uint32_t *r, uint32_t *sz) {
+  const uint32_t b0 = p[0];
+  *r = 0xFFFD;
+  *sz = 1;
+  auto cont = [&](uint64_t i) { return i < n && (p[i] & 0xC0) == 0x80; };
+  if (b0 < 0x80) {
+    *r = b0;
+  } else if (b0 >= 0xC2 && b0 <= 0xDF) {
+    if (cont(1)) {
+      *r = ((b0 & 0x1F) << 6) | (p[1] & 0x3F);
+      *sz = 2;
+    }
+  } else if (b0 >= 0xE0 && b0 <= 0xEF) {
+    if (cont(1) && cont(2) && !(b0 == 0xE0 && p[1] < 0xA0) &&
+        !(b0 == 0xED && p[1] > 0x9F)) {
+      *r = ((b0 & 0x0F) << 12) | (uint32_t(p[1] & 0x3F) << 6) | (p[2] & 0x3F);
+      *sz = 3;
+    }
+  } else if (b0 >= 0xF0 && b0 <= 0xF4) {
+    if (cont(1) && cont(2) && cont(3) && !(b0 == 0xF0 && p[1] < 0x90) &&
+        !(b0 == 0xF4 && p[1] > 0x8F)) {
+      *r = ((b0 & 0x07) << 18) | (uint32_t(p[1] & 0x3F) << 12) |
+           (uint32_t(p[2] & 0x3F) << 6) | (p[3] & 0x3F);
+      *sz = 4;
+    }
+  }
+}
+
+// Byte sink: counts, and writes when out != nullptr (LDS or global, through
+// a generic pointer).
+struct Sink {
+  uint8_t *out;
+  uint32_t o;
+  __device__ __forceinline__ void put(uint8_t c) {
+    if (out) out[o] = c;
+    ++o;
+  }
+  __device__ __forceinline__ void lit(const char *s) {
+    for (; *s; ++s) put(uint8_t(*s));
+  }
+};
+
+__device__ void json_string(Sink &k, const uint8_t *s, uint64_t n) {
+  k.put('"');
+  for (uint64_t i = 0; i < n;) {
+    const uint8_t b = s[i];
+    if (b < 0x80) {
+      if (b >= 0x20 && b != '"' && b != '\\' && b != '<' && b != '>' && b != '&') {
+        k.put(b);
+      } else {
+        k.put('\\');
+        switch (b) {
+          case '"': case '\\': k.put(b); break;
+          case '\b': k.put('b'); break;
+          case '\f': k.put('f'); break;
+          case '\n': k.put('n'); break;
+          case '\r': k.put('r'); break;
+          case '\t': k.put('t'); break;
+          default:
+            k.put('u'); k.put('0'); k.put('0');
+            k.put(uint8_t(kHexD[b >> 4])); k.put(uint8_t(kHexD[b & 15]));
+        }
+      }
+      ++i;
+      continue;
+    }
+    uint32_t r, sz;
+    decode_rune(s + i, n - i, &r, &sz);
+    if (r == 0xFFFD && sz == 1) {
+      k.lit("\\ufffd");
+    } else if (r == 0x2028 || r == 0x2029) {
+      k.lit("\\u202");
+      k.put(uint8_t(kHexD[r & 15]));
+    } else {
+      for (uint32_t q = 0; q < sz; ++q) k.put(s[i + q]);
+    }
+    i += sz;
+  }
+  k.put('"');
+}
+
+__device__ void dec(Sink &k, uint64_t v) {
+  uint8_t t[20];
+  int c = 0;
+  do {
+    t[c++] = uint8_t('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (c) k.put(t[--c]);
+}
+
+__device__ void hex32(Sink &k, const uint8_t *x) {
+  k.put('"');
+  for (int i = 0; i < 32; ++i) {
+    k.put(uint8_t(kHexD[x[i] >> 4]));
+    k.put(uint8_t(kHexD[x[i] & 15]));
+  }
+  k.put('"');
+}
+
+__device__ uint32_t line(const TArgs &a, uint64_t i, uint8_t *out) {
+  Sink k{out, 0};
+  k.lit("{\"name\":");
+  json_string(k, a.names + a.name_offs[i], a.name_offs[i + 1] - a.name_offs[i]);
+  k.lit(",\"mode\":");
+  dec(k, a.modes[i]);
+  k.lit(",\"ref\":{\"type\":");
+  json_string(k, a.types + a.type_offs[i], a.type_offs[i + 1] - a.type_offs[i]);
+  k.lit(",\"cid\":");
+  hex32(k, a.roots + 64 * i);
+  k.lit(",\"dek\":");
+  hex32(k, a.roots + 64 * i + 32);
+  k.lit(",\"size\":");
+  dec(k, a.sizes[i]);
+  k.lit(",\"blockSize\":");
+  dec(k, a.block_sizes[i]);
+  k.lit("}}\n");
+  return k.o;
+}
+
+__global__ __launch_bounds__(256) void k_tree_len(TArgs a) {
+  __shared__ uint64_t s[256];
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  uint64_t v = i < a.n ? line(a, i, nullptr) : 0;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint64_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
+    __syncthreads();
+    v += add;
+    s[threadIdx.x] = v;
+    __syncthreads();
+  }
+  if (i < a.n) a.local_end[i] = v;
+  if (threadIdx.x == 255) a.wg_total[blockIdx.x] = v;
+}
+
+// One workgroup: wg_total[0..m) -> exclusive prefix, in chunks of 1024.
+__global__ __launch_bounds__(1024) void k_tree_prefix(uint64_t *t, uint64_t m,
+                                                      uint64_t *total) {
+  __shared__ uint64_t s[1024];
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < m; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t x = i < m ? t[i] : 0;
+    uint64_t v = x;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+      const uint64_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
+      __syncthreads();
+      v += add;
+      s[threadIdx.x] = v;
+      __syncthreads();
+    }
+    if (i < m) t[i] = carry + v - x;
+    carry += s[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_tree_write(TArgs a) {
+  __shared__ uint4 img4[kImg / 16];
+  uint8_t *img = reinterpret_cast<uint8_t *>(img4);
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t last = min<uint64_t>(uint64_t(blockIdx.x) * 256 + 255, a.n - 1);
+  const uint64_t base = a.wg_total[blockIdx.x];   // exclusive prefix
+  const uint64_t span = a.local_end[last];        // this workgroup's bytes
+  const uint32_t sh = uint32_t((reinterpret_cast<uintptr_t>(a.out) + base) & 15);
+  if (*a.total > a.cap) return;  // uniform: the caller reports the error
+  const uint64_t end = i < a.n ? a.local_end[i] : 0;
+  const uint64_t start = (i < a.n && threadIdx.x) ? a.local_end[i - 1] : 0;
+  if (i < a.n && a.line_ends) a.line_ends[i] = base + end;
+  if (span + sh > kImg) {  // uniform: lines too long for the image
+    if (i < a.n) line(a, i, a.out + base + start);
+    return;
+  }
+  if (i < a.n) line(a, i, img + sh + start);
+  __syncthreads();
+  // image byte x <-> out byte base - sh + x; granules [16g, 16g+16)
+  uint8_t *dst = a.out + base - sh;
+  const uint32_t tot = uint32_t(span) + sh;
+  const uint32_t ng = (tot + 15) / 16;
+  for (uint32_t g = threadIdx.x; g < ng; g += 256) {
+    const uint32_t lo = 16 * g, hi = lo + 16;
+    if (lo >= sh && hi <= tot) {
+      *reinterpret_cast<uint4 *>(dst + lo) = img4[g];
+    } else {
+      for (uint32_t x = max(lo, sh); x < min(hi, tot); ++x) dst[x] = img[x];
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// n blobs of len bytes (len % 8 == 0) back to back: byte o of blob b =
+// byte (o & 7) of splitmix64((seed0 + b) ^ (o >> 3)), i.e. blob b is the
+// splitmix stream of seed seed0 + b (oracle_fill_splitmix_blobs).
+__global__ __launch_bounds__(256) void k_fill_blobs(uint64_t *dst, uint64_t n,
+                                                    uint64_t words, uint64_t seed0) {
+  const uint64_t total = n * words;
+  for (uint64_t w = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; w < total;
+       w += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t b = w / words, k = w - b * words;
+    dst[w] = splitmix64((seed0 + b) ^ k);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
+  if (j.n == 0) return hipSuccess;
+  TArgs a{};
+  a.n = j.n;
+  a.names = j.names;
+  a.name_offs = j.name_offs;
+  a.modes = j.modes;
+  a.types = j.types;
+  a.type_offs = j.type_offs;
+  a.roots = j.roots;
+  a.sizes = j.sizes;
+  a.block_sizes = j.block_sizes;
+  a.local_end = j.scratch;
+  const uint64_t wgs = (j.n + 255) / 256;
+  a.wg_total = j.scratch + j.n;
+  a.line_ends = j.line_ends;
+  a.out = j.out;
+  a.cap = j.cap;
+  a.total = j.total;
+  hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
+                     j.total);
+  e = hipGetLastError();
+  if (e != hipSuccess || !j.out) return e;
+  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_blobs(uint8_t *dst, uint64_t n, uint64_t len, uint64_t seed0,
+                             hipStream_t s) {
+  if (n == 0 || len == 0) return hipSuccess;
+  if (len % 8 || (reinterpret_cast<uintptr_t>(dst) & 7)) return hipErrorInvalidValue;
+  const uint64_t words = n * (len / 8);
+  uint64_t grid = (words + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(k_fill_blobs, dim3(uint32_t(grid)), dim3(256), 0, s,
+                     reinterpret_cast<uint64_t *>(dst), n, len / 8, seed0);
+  return hipGetLastError();
+}
+
+}  // namespace glfsx

@@ -77,9 +77,9 @@ class Machine:
         """machine.go:50-54."""
         return bigblob.derive_key(self.salt, ty.encode())
 
-    def new_typed_writer(self, store, ty: str) -> TypedWriter:
-        """glfs.go:74-76."""
-        return TypedWriter(ty, self.bbag.new_writer(store, self.make_salt(ty)))
+    def new_typed_writer(self, store, ty: str, strict: bool = False) -> TypedWriter:
+        """glfs.go:74-76 (strict: the reference's per-Write error timing)."""
+        return TypedWriter(ty, self.bbag.new_writer(store, self.make_salt(ty), strict=strict))
 
     def post_typed(self, store, ty: str, r) -> Ref:
         """glfs.go:50-57."""
@@ -95,9 +95,10 @@ class Machine:
         return self.post_typed(store, TYPE_BLOB, r)
 
     def post_blobs(self, store, blobs) -> list:
-        """n sequential PostBlob calls (machine.go:64-66) for blobs that each
-        fit one block, batched into one GPU launch pair (one lane per blob).
-        The store sees the same Posts in the same order."""
+        """n sequential PostBlob calls (machine.go:64-66), batched: blobs of
+        at most 16 KiB share one GPU launch pair (one lane per blob), larger
+        ones go through the Writer.  The store sees the same Posts in the
+        same order."""
         import ctypes
         from . import _native as N
         blobs = [bytes(b) for b in blobs]
@@ -120,7 +121,8 @@ class Machine:
         if rc == N.GLFSX_E_STORE and errors:
             raise bigblob.StoreError(rc, repr(errors[0])) from errors[0]
         N.check(rc)
-        return [Ref(TYPE_BLOB, Root(bigblob.Ref.from_bytes(roots.raw[64 * i:64 * i + 64]),
+        rr = roots.raw   # (.raw copies the whole buffer on every access)
+        return [Ref(TYPE_BLOB, Root(bigblob.Ref(rr[64 * i:64 * i + 32], rr[64 * i + 32:64 * i + 64]),
                                     lens[i], self.block_size)) for i in range(n)]
 
     def new_blob_writer(self, store) -> TypedWriter:

@@ -104,8 +104,8 @@ def is_valid_name(x: str) -> bool:
 
 
 def _name_key(name: str) -> bytes:
-    # strings.Compare is byte-wise on the UTF-8 encoding
-    return name.encode("utf-8", "surrogatepass")
+    # strings.Compare is byte-wise on the Go string's bytes
+    return go_bytes(name)
 
 
 def sort_tree_entries(ents: list) -> None:
@@ -145,17 +145,28 @@ _ESC = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t",
         "\u2028": "\\u2028", "\u2029": "\\u2029"}
 
 
+def go_bytes(s: str) -> bytes:
+    """A Go string's bytes from its Python mirror: undecodable bytes ride in
+    a str as surrogate escapes (U+DC80..U+DCFF); other lone surrogates are
+    kept as their (invalid) 3-byte encodings."""
+    try:
+        return s.encode("utf-8", "surrogateescape")
+    except UnicodeEncodeError:
+        return s.encode("utf-8", "surrogatepass")
+
+
 def go_json_string(s: str) -> str:
-    """encoding/json string encoding with HTML escaping (Encoder default)."""
+    """encoding/json appendString with escapeHTML (the Encoder default):
+    invalid UTF-8 becomes the 6-byte escape \\ufffd, one per bad byte."""
     out = ['"']
-    for ch in s:
+    for ch in go_bytes(s).decode("utf-8", "surrogateescape"):
         e = _ESC.get(ch)
         if e is not None:
             out.append(e)
         elif ch < " ":
             out.append("\\u%04x" % ord(ch))
-        elif 0xD800 <= ord(ch) <= 0xDFFF:  # a lone surrogate = invalid UTF-8
-            out.append("\ufffd")
+        elif 0xD800 <= ord(ch) <= 0xDFFF:  # an undecodable byte
+            out.append("\\ufffd")
         else:
             out.append(ch)
     out.append('"')
@@ -183,6 +194,48 @@ def entry_json_line(te: TreeEntry, cid_json: Callable[[bytes], str] = cid_json_h
     return s.encode("utf-8")
 
 
+def encode_lines(ents, cid_json: Callable[[bytes], str] = cid_json_hex):
+    """The JSON lines of `ents` in order, and each line's end offset.  The
+    default cid form is encoded natively (glfsx_tree_encode: host C++,
+    multi-threaded, byte-identical to entry_json_line); a custom cid_json
+    goes through entry_json_line."""
+    import ctypes
+    from . import _native as N
+    n = len(ents)
+    if cid_json is not cid_json_hex or n == 0:
+        lines = [entry_json_line(e, cid_json) for e in ents]
+        ends, acc = [], 0
+        for ln in lines:
+            acc += len(ln)
+            ends.append(acc)
+        return b"".join(lines), ends
+    names = [go_bytes(e.name) for e in ents]
+    types = [go_bytes(e.ref.type) for e in ents]
+    U64 = ctypes.c_uint64 * (n + 1)
+
+    def offs(parts):
+        o, acc = [0], 0
+        for p in parts:
+            acc += len(p)
+            o.append(acc)
+        return U64(*o)
+
+    modes = (ctypes.c_uint32 * n)(*[e.file_mode for e in ents])
+    roots = b"".join(e.ref.root.ref.cid + e.ref.root.ref.dek for e in ents)
+    sizes = (ctypes.c_uint64 * n)(*[e.ref.root.size for e in ents])
+    bss = (ctypes.c_uint64 * n)(*[e.ref.root.block_size for e in ents])
+    nb, tb = b"".join(names), b"".join(types)
+    no, to = offs(names), offs(types)
+    total = ctypes.c_uint64()
+    ends = (ctypes.c_uint64 * n)()
+    N.check(N.lib.glfsx_tree_encode(n, nb, no, modes, tb, to, roots, sizes, bss, None, 0,
+                                    ctypes.byref(total), ends))
+    out = ctypes.create_string_buffer(max(total.value, 1))
+    N.check(N.lib.glfsx_tree_encode(n, nb, no, modes, tb, to, roots, sizes, bss, out,
+                                    total.value, ctypes.byref(total), ends))
+    return out.raw[:total.value], list(ends)
+
+
 def _cid_from_json(v) -> bytes:
     if isinstance(v, str):
         return bytes.fromhex(v)
@@ -199,48 +252,54 @@ def entry_from_json(obj: dict, cid_from_json=_cid_from_json) -> TreeEntry:
 # ------------------------------------------------------------------ writer
 class TreeWriter:
     """tree.go:284-320.  Put checks order and referential integrity, then
-    json-encodes the entry into a TypedWriter("tree").  Lines are handed to
-    the bigblob Writer in runs that end exactly where the reference's Writer
-    would post a chunk, so a store error surfaces at the same Put."""
+    json-encodes the entry into a TypedWriter("tree").  The typed writer runs
+    in strict mode, so a store error surfaces at the same Put as in the
+    reference (the Put whose line completes the failing block)."""
 
     def __init__(self, machine: "glfs.Machine", store,
                  cid_json: Callable[[bytes], str] = cid_json_hex):
         self.dst = store
-        self.tw = machine.new_typed_writer(store, glfs.TYPE_TREE)
+        self.tw = machine.new_typed_writer(store, glfs.TYPE_TREE, strict=True)
         self.cid_json = cid_json
         self.last_name = ""
-        self._pending: list = []
-        self._pending_len = 0
-        self._written = 0
-        self._bs = machine.block_size
+
+    def _check(self, te: TreeEntry, last: str) -> None:
+        if _name_key(te.name) <= _name_key(last):
+            raise TreeError(f"cannot write tree entries out of order "
+                            f"{te.name!r} <= {last!r}")
+        if not exists_unit(self.dst, te.ref.root.ref.cid):
+            raise TreeError(f"adding tree ent {te} would violate referential integrity")
 
     def put(self, te: TreeEntry) -> None:
         """tree.go:295-312."""
-        if _name_key(te.name) <= _name_key(self.last_name):
-            raise TreeError(f"cannot write tree entries out of order "
-                            f"{te.name!r} <= {self.last_name!r}")
-        if not exists_unit(self.dst, te.ref.root.ref.cid):
-            raise TreeError(f"adding tree ent {te} would violate referential integrity")
-        line = entry_json_line(te, self.cid_json)
-        self._pending.append(line)
-        self._pending_len += len(line)
-        # the reference Writer posts when its buffer reaches a block: flush
-        # everything pending on the Put that crosses a block boundary
-        if (self._written + self._pending_len) // self._bs > self._written // self._bs:
-            self._flush()
+        self._check(te, self.last_name)
+        self.tw.write(entry_json_line(te, self.cid_json))
         self.last_name = te.name
 
-    def _flush(self) -> None:
-        if self._pending:
-            data = b"".join(self._pending)
-            self._pending, self._pending_len = [], 0
+    def put_many(self, ents) -> None:
+        """Put each entry in order (tree.go:295-312), batched: the entries
+        before the first failing check are encoded at once (natively) and
+        written, then that check's error is raised -- the same bytes reach
+        the Writer as with one Put per entry."""
+        ents = list(ents)
+        err, k, last = None, len(ents), self.last_name
+        for i, te in enumerate(ents):
+            try:
+                self._check(te, last)
+            except TreeError as e:
+                err, k = e, i
+                break
+            last = te.name
+        if k:
+            data, _ = encode_lines(ents[:k], self.cid_json)
             self.tw.write(data)
-            self._written += len(data)
+            self.last_name = ents[k - 1].name
+        if err is not None:
+            raise err
 
     def finish(self) -> glfs.Ref:
         """tree.go:315-317."""
         try:
-            self._flush()
             return self.tw.finish()
         finally:
             self.tw.bw.close()
@@ -273,8 +332,7 @@ def post_tree(machine: "glfs.Machine", store, ents: Iterable[TreeEntry],
     sort_tree_entries(root_ents)
     tw = TreeWriter(machine, store, cid_json)
     try:
-        for ent in root_ents:
-            tw.put(ent)
+        tw.put_many(root_ents)
     except BaseException:
         tw.tw.bw.close()
         raise

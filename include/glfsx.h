@@ -25,6 +25,7 @@
  *   glfsx_post_blobs*      glfs machine.go:64 PostBlob, batched over many
  *                          single-block blobs (tree.go:300-316 callers)
  *   glfsx_depth            bigblob/blob.go:256-264 depth()
+ *   glfsx_tree_encode      tree.go:300-316 TreeWriter.Put's JSON lines, batched
  *   glfsx_chacha20_xor*    bigblob/ref.go:137-144  cryptoXOR (read side decrypt)
  *
  * Conventions:
@@ -199,24 +200,59 @@ int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
                            uint64_t n1, uint64_t size, glfsx_root *out);
 
 /* --- many small blobs (glfs.PostBlob batched; BASELINE config 4) -------- */
-/* Blob i is data[offsets[i] .. offsets[i]+lengths[i]).  Every blob must fit
- * one bigblob block (0 <= len <= block_size; this kernel family also caps
- * len at 16 KiB), so its root is post(rawSalt, blob) (blob.go:190-193) or,
- * for an empty blob, post(indexSalt, "") (blob.go:187-189); rawSalt /
- * indexSalt derive from `salt` (glfs: the type salt, machine.go:50-54).
- * Writes 64-byte root refs (CID||DEK) per blob.  The host variant calls
- * `post` once per blob in order, like n sequential PostBlob calls. */
+/* n sequential glfs.PostBlob calls (machine.go:64) in one call: blob i is
+ * data[offsets[i] .. offsets[i]+lengths[i]).  A blob of at most one block
+ * has root post(rawSalt, blob) (blob.go:190-193), the empty blob
+ * post(indexSalt, "") (blob.go:187-189); rawSalt / indexSalt derive from
+ * `salt` (glfs: the type salt, machine.go:50-54).  Blobs of <= 16 KiB are
+ * hashed one lane each in one launch pair; larger ones (any size, several
+ * blocks included) go through the Writer.  Writes the 64-byte root ref
+ * (CID||DEK) per blob; `post` is called for every Post of blob 0, then blob
+ * 1, ... exactly as n sequential PostBlob calls would. */
 int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
                      const uint8_t *cid_key, const void *data,
                      const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
                      glfsx_post_fn post, void *post_ctx, uint8_t *roots_out);
 /* Device-resident: d_offsets / d_lengths are device arrays; max_len is the
- * largest length (caller-known).  Enqueued on stream, not synchronised. */
+ * largest length (caller-known; when it exceeds 16 KiB the lengths are read
+ * back and the larger blobs posted one by one, synchronising the stream).
+ * Enqueued on stream. */
 int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
                             const uint8_t *cid_key, const void *d_data,
                             const uint64_t *d_offsets, const uint64_t *d_lengths,
                             uint64_t n, uint64_t max_len, void *d_ctext,
                             void *d_roots, void *stream);
+
+/* --- tree blobs (tree.go:284-320; BASELINE config 4) -------------------- */
+/* TreeWriter.Put's json.Encoder.Encode(TreeEntry) (tree.go:300-316) for n
+ * entries at once, on host cores: line i =
+ *   {"name":N,"mode":M,"ref":{"type":T,"cid":"<hex>","dek":"<hex>",
+ *    "size":S,"blockSize":B}}\n
+ * with encoding/json's string escaping (HTML-safe, invalid UTF-8 as \ufffd).
+ * names / types: concatenated bytes, name_offs / type_offs: n+1 offsets;
+ * roots: 64-byte CID||DEK per entry.  The cid field is written as a hex
+ * string (blobcache.CID's JSON form is not in the reference: parity
+ * unpinned).  Writes the lines to out (nullable: length only) and the total
+ * length to *out_len; line_ends (nullable) receives each line's end offset. */
+int glfsx_tree_encode(uint64_t n, const uint8_t *names, const uint64_t *name_offs,
+                      const uint32_t *modes, const uint8_t *types,
+                      const uint64_t *type_offs, const uint8_t *roots,
+                      const uint64_t *sizes, const uint64_t *block_sizes,
+                      uint8_t *out, uint64_t out_cap, uint64_t *out_len,
+                      uint64_t *line_ends);
+
+/* The same lines encoded on the GPU from device-resident entries (d_roots
+ * typically the roots glfsx_post_blobs_device just wrote), into d_out
+ * (nullable: length only; nothing is written when the lines exceed out_cap,
+ * which returns GLFSX_E_ARG).  d_line_ends nullable.  Synchronises `stream`
+ * to return the total length in *out_len (host). */
+int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,
+                             const uint64_t *d_name_offs, const uint32_t *d_modes,
+                             const uint8_t *d_types, const uint64_t *d_type_offs,
+                             const uint8_t *d_roots, const uint64_t *d_sizes,
+                             const uint64_t *d_block_sizes, void *d_out,
+                             uint64_t out_cap, uint64_t *d_line_ends,
+                             uint64_t *out_len, void *stream);
 
 /* --- read side (ref.go:113-126 getF decrypt) ---------- */
 /* ChaCha20, zero nonce, counter 0, key = dek (ref.go:137-144). */
@@ -230,6 +266,11 @@ int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
  * oracle_fill_splitmix.  Enqueued on stream (NULL = the thread's stream). */
 int glfsx_fill_splitmix_device(void *d_dst, uint64_t offset, uint64_t n,
                                uint64_t seed, void *stream);
+
+/* n blobs of len bytes back to back (len % 8 == 0): blob b is the stream
+ * above with seed seed0 + b at offset 0 (config 4: seed = blob index). */
+int glfsx_fill_splitmix_blobs_device(void *d_dst, uint64_t n, uint64_t len,
+                                     uint64_t seed0, void *stream);
 
 /* A glfsx_post_fn that only counts: ctx points at uint64_t[2] = {posts,
  * bytes}.  For benchmarks of the host round trip without a store. */

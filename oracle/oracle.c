@@ -566,3 +566,10 @@ void oracle_fill_splitmix(uint8_t *dst, uint64_t offset, uint64_t n,
     dst[i] = (uint8_t)(w >> (8 * (o & 7)));
   }
 }
+
+/* n blobs of len bytes back to back: blob b = oracle_fill_splitmix(seed0 + b)
+ * at offset 0 (BASELINE config 4: distinct blobs, seed = blob index). */
+void oracle_fill_splitmix_blobs(uint8_t *dst, uint64_t n, uint64_t len,
+                                uint64_t seed0) {
+  for (uint64_t b = 0; b < n; b++) oracle_fill_splitmix(dst + b * len, 0, len, seed0 + b);
+}

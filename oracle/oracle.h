@@ -105,6 +105,11 @@ void oracle_post_batch(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
 void oracle_fill_splitmix(uint8_t *dst, uint64_t offset, uint64_t n,
                           uint64_t seed);
 
+/* n blobs of len bytes back to back, blob b = the stream above with seed
+ * seed0 + b at offset 0 (config 4: seed = blob index). */
+void oracle_fill_splitmix_blobs(uint8_t *dst, uint64_t n, uint64_t len,
+                                uint64_t seed0);
+
 #ifdef __cplusplus
 }
 #endif

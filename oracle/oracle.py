@@ -54,6 +54,8 @@ def lib():
                                         c_u8p, ctypes.c_int]
         L.oracle_fill_splitmix.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
                                            ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_fill_splitmix_blobs.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_uint64]
         _lib = L
     return _lib
 

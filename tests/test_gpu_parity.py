@@ -713,3 +713,49 @@ def test_concat_vs_oracle(gpu, O):
     want = O.create(b"".join(parts), bs, salt=None)[0]
     assert got.ref.marshal_binary() == want
     assert got.size == sum(map(len, parts))
+
+
+def test_post_blobs_mixed_sizes(gpu, O):
+    """glfs.PostBlob batched over blobs of every size class: <= 16 KiB (one
+    lane each), one block above 16 KiB, exactly one block, and several
+    blocks (a whole Create with an index node): every root and the whole
+    Post sequence equal n sequential reference PostBlob calls."""
+    import torch
+    from glfs_amd import _native as N, bigblob, glfs
+    bs = 2 << 20
+    lens = [0, 5, 16384, 16385, 100_000, bs - 1, bs, bs + 1, 3 * bs + 5, 4096, 0, 77]
+    blobs = [O.fill_splitmix(n, 300 + i) for i, n in enumerate(lens)]
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    store = bigblob.MemStore(bs)
+    refs = glfs.Machine().post_blobs(store, blobs)
+    want_log = []
+    for i, b in enumerate(blobs):
+        want, size, _, posts = O.create(b, bs, salt=blob_salt)
+        assert refs[i].root.ref.marshal_binary() == want, (i, len(b))
+        assert refs[i].root.size == len(b)
+        want_log += [(k, r) for k, r, _, _ in posts]
+    assert [(k, r) for k, r, _ in store.log] == want_log
+    # device-resident: the same roots, ctext of every blob in place
+    offs, pos = [], 0
+    for b in blobs:
+        offs.append(pos)
+        pos += len(b) + 13          # unaligned, gaps between blobs
+    d = torch.zeros(pos + 64, dtype=torch.uint8, device="cuda")
+    for o, b in zip(offs, blobs):
+        if b:
+            d[o:o + len(b)] = torch.tensor(list(b), dtype=torch.uint8, device="cuda") \
+                if len(b) < 100_000 else torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    roots = torch.zeros(64 * len(blobs), dtype=torch.uint8, device="cuda")
+    ct = torch.zeros_like(d)
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(lens, dtype=torch.int64, device="cuda")
+    N.check(N.lib.glfsx_post_blobs_device(bs, blob_salt, None, d.data_ptr(), do.data_ptr(),
+                                          dl.data_ptr(), len(blobs), max(lens), ct.data_ptr(),
+                                          roots.data_ptr(), None))
+    torch.cuda.synchronize()
+    rh = bytes(roots.cpu().numpy().tobytes())
+    cth = bytes(ct.cpu().numpy().tobytes())
+    for i, b in enumerate(blobs):
+        assert rh[64 * i:64 * i + 64] == refs[i].root.ref.marshal_binary(), i
+        if 0 < len(b) <= bs:
+            assert cth[offs[i]:offs[i] + len(b)] == O.post(O.derive_key(blob_salt, b"raw"), b)[1]

@@ -220,3 +220,175 @@ def test_sync_and_populate(gpu, O):
     order = []
     m.traverse(src, root, lambda cid: True, lambda lvl, ref: order.append(lvl))
     assert order[-1] == bigblob.depth(root.size, bs) and order.count(0) == 49
+
+
+# ------------------------------------------------------ config 4, full size
+def _dev_arr(torch, vals, dtype):
+    return torch.tensor(vals, dtype=dtype, device="cuda")
+
+
+def _encode_device(torch, ents, out_shift=0, cap=None, want_ends=True):
+    """glfsx_tree_encode_device over entries copied to HBM; returns (bytes,
+    line_ends) or raises GlfsxError."""
+    import ctypes
+    from glfs_amd import _native as N, tree as T
+    n = len(ents)
+    names = [T.go_bytes(e.name) for e in ents]
+    types = [T.go_bytes(e.ref.type) for e in ents]
+
+    def offs(parts):
+        o, acc = [0], 0
+        for p in parts:
+            acc += len(p)
+            o.append(acc)
+        return o
+
+    u8 = lambda b: torch.tensor(list(b) or [0], dtype=torch.uint8, device="cuda")
+    d_names, d_types = u8(b"".join(names)), u8(b"".join(types))
+    d_no, d_to = _dev_arr(torch, offs(names), torch.int64), _dev_arr(torch, offs(types), torch.int64)
+    d_modes = _dev_arr(torch, [e.file_mode for e in ents], torch.int64).to(torch.int32)
+    d_roots = u8(b"".join(e.ref.root.ref.cid + e.ref.root.ref.dek for e in ents))
+    d_sizes = _dev_arr(torch, [e.ref.root.size for e in ents], torch.int64)
+    d_bss = _dev_arr(torch, [e.ref.root.block_size for e in ents], torch.int64)
+    total = ctypes.c_uint64()
+    N.check(N.lib.glfsx_tree_encode_device(n, d_names.data_ptr(), d_no.data_ptr(),
+                                           d_modes.data_ptr(), d_types.data_ptr(),
+                                           d_to.data_ptr(), d_roots.data_ptr(),
+                                           d_sizes.data_ptr(), d_bss.data_ptr(), None, 0,
+                                           None, ctypes.byref(total), None))
+    ln = total.value
+    out = torch.full((ln + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    ends = torch.zeros(n, dtype=torch.int64, device="cuda")
+    rc = N.lib.glfsx_tree_encode_device(n, d_names.data_ptr(), d_no.data_ptr(),
+                                        d_modes.data_ptr(), d_types.data_ptr(),
+                                        d_to.data_ptr(), d_roots.data_ptr(),
+                                        d_sizes.data_ptr(), d_bss.data_ptr(),
+                                        out.data_ptr() + out_shift,
+                                        ln if cap is None else cap,
+                                        ends.data_ptr() if want_ends else None,
+                                        ctypes.byref(total), None)
+    torch.cuda.synchronize()
+    o = bytes(out.cpu().numpy().tobytes())
+    if rc:
+        assert set(o) == {0xA5}, "nothing may be written on error"
+        N.check(rc)
+    assert set(o[:out_shift]) <= {0xA5} and set(o[out_shift + ln:]) <= {0xA5}
+    return o[out_shift:out_shift + ln], ends.cpu().tolist()
+
+
+def test_tree_encode_device_vs_host(gpu):
+    """k_tree_len/prefix/write == the host encoder == entry_json_line, for
+    every escaping class, several destination alignments, lines too long
+    for a workgroup's LDS image, and a too-small buffer (an error, nothing
+    written)."""
+    import torch
+    from glfs_amd import _native as N, bigblob, glfs, tree as T
+    rng = random.Random(17)
+    pool = ["plain", "<a&b>", "\n\r\t\b\f\x00\x1f\x7f", "é日本\U0001F600", "bad\udc80\udcff",
+            "q\"b\\s", " x ", "%07d" % 5, "\udced\udca0\udc80"]
+    ents = []
+    for i in range(3000):
+        name = rng.choice(pool) + str(i) + rng.choice(pool)
+        if i % 700 == 3:
+            name = "L" * rng.randrange(300, 2000) + name   # forces the byte path
+        r = glfs.Ref(rng.choice(["blob", "tree", "<&>"]),
+                     bigblob.Root(bigblob.Ref(rng.randbytes(32), rng.randbytes(32)),
+                                  rng.randrange(1 << 63), rng.choice([128, 2 << 20])))
+        ents.append(T.TreeEntry(name, rng.choice([0o644, T.MODE_TREE]), r))
+    want, want_ends = T.encode_lines(ents)
+    assert want == b"".join(T.entry_json_line(e) for e in ents)
+    for shift in (0, 1, 7, 15):
+        got, ends = _encode_device(torch, ents, out_shift=shift)
+        assert got == want, shift
+        assert ends == want_ends
+    with pytest.raises(N.GlfsxError):
+        _encode_device(torch, ents, cap=len(want) - 1)
+
+
+def test_fill_blobs_matches_oracle(gpu, O):
+    import ctypes
+    import torch
+    from glfs_amd import _native as N
+    n, ln = 1000, 4096
+    t = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_fill_splitmix_blobs_device(t.data_ptr(), n, ln, 17, None))
+    torch.cuda.synchronize()
+    want = ctypes.create_string_buffer(n * ln)
+    O.lib().oracle_fill_splitmix_blobs(want, n, ln, 17)
+    assert bytes(t.cpu().numpy().tobytes()) == want.raw
+    assert want.raw[5 * ln:6 * ln] == O.fill_splitmix(ln, 22)
+
+
+def test_config4_full_size_end_to_end(gpu, O):
+    """BASELINE config 4 at its stated size: 1,048,576 distinct 4 KiB blobs
+    (blob i = splitmix stream of seed i) -> glfs.Machine.post_blobs (the
+    store receives every Post in order) -> PostTreeMap with "%07d" names.
+    Every one of the 1M roots vs the threaded oracle; the tree root vs the
+    oracle's Create of the tree bytes (encoded by entry_json_line, an
+    independent encoder) under typeSalt("tree").  Then the device-resident
+    route (post_blobs_device -> tree_encode_device -> create_device) must
+    give the same tree root."""
+    import ctypes
+    import numpy as np
+    import torch
+    from glfs_amd import _native as N, bigblob, glfs, tree as T
+    n, ln, bs = 1 << 20, 4096, 2 * MIB
+    d = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_fill_splitmix_blobs_device(d.data_ptr(), n, ln, 0, None))
+    torch.cuda.synchronize()
+    host = d.cpu().numpy()
+    hb = host.tobytes()
+    blobs = [hb[i * ln:(i + 1) * ln] for i in range(n)]
+    # ------------------------------------------------ the Python API route
+    s = bigblob.MemStore(bs)
+    m = glfs.Machine()
+    refs = m.post_blobs(s, blobs)
+    print("config4: posted", n, "blobs", flush=True)
+    assert len(s.log) == n
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    raw = O.derive_key(blob_salt, b"raw")
+    want = np.empty(64 * n, dtype=np.uint8)
+    O.lib().oracle_post_batch(want.ctypes.data, None, raw, host.ctypes.data, n * ln, ln,
+                              None, 16)
+    want_b = want.tobytes()
+    got_b = b"".join(r.root.ref.marshal_binary() for r in refs)
+    assert got_b == want_b                       # every root, bit-exact
+    assert all(r.root.size == ln and r.root.block_size == bs for r in refs)
+    assert [k for k, _, _ in s.log[:3]] == [0, 0, 0]
+    assert s.log[n - 1][1] == want_b[64 * (n - 1):]
+    del blobs
+    tref = m.post_tree_map(s, {"%07d" % i: r for i, r in enumerate(refs)})
+    print("config4: tree posted", flush=True)
+    ents = [T.TreeEntry("%07d" % i, 0o644, r) for i, r in enumerate(refs)]
+    tree_bytes = b"".join(T.entry_json_line(e) for e in ents)
+    tsalt = O.derive_key(bytes(32), b"tree")
+    want_root, size, _, want_posts = O.create(tree_bytes, bs, salt=tsalt, store_max=bs)
+    assert tref.root.ref.marshal_binary() == want_root
+    assert tref.root.size == size == len(tree_bytes)
+    assert [r for _, r, _ in s.log[n:]] == [r for _, r, _, _ in want_posts]
+    # --------------------------------------------- the device-resident route
+    roots = torch.empty(64 * n, dtype=torch.uint8, device="cuda")
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * ln
+    lens = torch.full((n,), ln, dtype=torch.int64, device="cuda")
+    N.check(N.lib.glfsx_post_blobs_device(bs, blob_salt, None, d.data_ptr(), offs.data_ptr(),
+                                          lens.data_ptr(), n, ln, None, roots.data_ptr(), None))
+    names = torch.tensor(np.frombuffer("".join("%07d" % i for i in range(n)).encode(),
+                                       dtype=np.uint8), device="cuda")
+    name_offs = torch.arange(n + 1, dtype=torch.int64, device="cuda") * 7
+    types = torch.tensor(np.frombuffer(b"blob" * n, dtype=np.uint8), device="cuda")
+    type_offs = torch.arange(n + 1, dtype=torch.int64, device="cuda") * 4
+    modes = torch.full((n,), 0o644, dtype=torch.int32, device="cuda")
+    bss = torch.full((n,), bs, dtype=torch.int64, device="cuda")
+    out = torch.empty(len(tree_bytes) + 64, dtype=torch.uint8, device="cuda")
+    total = ctypes.c_uint64()
+    N.check(N.lib.glfsx_tree_encode_device(n, names.data_ptr(), name_offs.data_ptr(),
+                                           modes.data_ptr(), types.data_ptr(),
+                                           type_offs.data_ptr(), roots.data_ptr(),
+                                           lens.data_ptr(), bss.data_ptr(), out.data_ptr(),
+                                           out.numel(), None, ctypes.byref(total), None))
+    assert total.value == len(tree_bytes)
+    assert bytes(out[:total.value].cpu().numpy().tobytes()) == tree_bytes
+    r = N.glfsx_root()
+    N.check(N.lib.glfsx_create_device(bs, tsalt, None, out.data_ptr(), total.value, None,
+                                      ctypes.byref(r), None, None))
+    assert bytes(r.ref) == want_root

@@ -18,7 +18,8 @@ def _ref(ty="blob", size=9, bs=2 << 20, c=0x11, d=0x22):
     ("\x00\x01\x1f", '"\\u0000\\u0001\\u001f"'),
     ("\u2028\u2029", '"\\u2028\\u2029"'),
     ("é日本\U0001F600", '"é日本\U0001F600"'),
-    ("bad\udc80", '"bad\ufffd"'),
+    ("bad\udc80", '"bad\\ufffd"'),
+    ("a\udcff\udc80b", '"a\\ufffd\\ufffdb"'),
     ("\x7f", '"\x7f"'),
 ])
 def test_go_json_string(s, want):
@@ -77,3 +78,27 @@ def test_read_tree_bytes_roundtrip_and_order():
     with pytest.raises(T.TreeError, match="out of order"):
         T.read_tree_bytes(bad)
     assert T.read_tree_bytes(b"") == []
+
+
+def test_native_encoder_matches_python():
+    """glfsx_tree_encode (host C++, multi-threaded; no GPU) writes the same
+    bytes as entry_json_line for every escaping class, line by line."""
+    import random
+    rng = random.Random(7)
+    pool = ["plain", "<a&b>", "\n\r\t\b\f\x00\x1f\x7f", " x ", "é日本\U0001F600",
+            "bad\udc80\udcff", "q\"b\\s", "", "%07d" % 5, "\udced\udca0\udc80"]
+    ents = []
+    for i in range(20000):
+        name = rng.choice(pool) + str(i) + rng.choice(pool)
+        ty = rng.choice(["blob", "tree", "t<&>", " "])
+        r = glfs.Ref(ty, bigblob.Root(bigblob.Ref(rng.randbytes(32), rng.randbytes(32)),
+                                      rng.randrange(1 << 62), rng.choice([128, 2 << 20])))
+        ents.append(T.TreeEntry(name, rng.choice([0o644, T.MODE_TREE, 0]), r))
+    data, ends = T.encode_lines(ents)
+    want = [T.entry_json_line(e) for e in ents]
+    assert data == b"".join(want)
+    acc = 0
+    for ln, e in zip(want, ends):
+        acc += len(ln)
+        assert e == acc
+    assert T.encode_lines([]) == (b"", [])
