@@ -63,7 +63,7 @@ def parse():
                    help="do not write ctext (NOT the headline configuration)")
     p.add_argument("--no-extras", action="store_true",
                    help="skip roofline/cpu/host legs (profiling runs)")
-    p.add_argument("--cpu-sample-mib", type=int, default=1024)
+    p.add_argument("--cpu-sample-mib", type=int, default=3072)
     p.add_argument("--host-rt-gib", type=float, default=4.0)
     return p.parse_args()
 
@@ -117,20 +117,10 @@ def main():
                                               ctypes.byref(root), ctypes.byref(n_posts), sp))
             root_ref[0] = bytes(root.ref)
             return
-        lvl1 = shard.shard_device(N, bs, None, None, data.data_ptr(), total, first, nb,
-                                  ct_ptr, sp)
-        mine = torch.frombuffer(bytearray(lvl1), dtype=torch.uint8)
-        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64))
-        cap = int(max(t.item() for t in sizes))
-        padded = torch.zeros(cap, dtype=torch.uint8)
-        padded[:mine.numel()] = mine
-        gathered = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(gathered, padded)   # the only exchange: 64 B per bf blocks
+        _, r = shard.write_sharded(N, dist, bs, None, None, data.data_ptr(), total, first, nb,
+                                   ct_ptr, sp)
         if rank == 0:
-            allrefs = b"".join(bytes(g[:int(n.item())].numpy().tobytes())
-                               for g, n in zip(gathered, sizes))
-            root_ref[0] = shard.root_from_level1(N, bs, None, None, allrefs, total)
+            root_ref[0] = r
 
     def barrier():
         if world > 1:
@@ -176,7 +166,8 @@ def main():
 
     if not args.no_extras:
         if rank == 0:
-            out["roofline"], out["valu"] = roofline(torch, N, data, ctext, per, bs, stream, sp)
+            out["roofline"], out["valu"] = roofline(torch, N, data, ctext, per, bs, stream, sp,
+                                                    step_ms=ms, total_bytes=per)
         del ctext
         # host round trip on every rank at once (N PCIe links, N host feeders):
         # aggregate bytes over the slowest rank's time
@@ -205,7 +196,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
+def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, total_bytes=None):
     """Per-kernel average duration with HIP events on the launch stream: the
     DEK pass (reads ptext) and the ChaCha20+CID pass (reads ptext, writes
     ctext).  achieved = algorithmic bytes per launch / avg duration."""
@@ -246,23 +237,36 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
         rms = sum(tr[1:]) / reps
         read = {"value": round(per / GIB / (rms * 1e-3), 1), "unit": "GiB/s", "ms": round(rms, 3),
                 "what": "batched getF decrypt (ChaCha20 with each block's DEK), HBM->HBM"}
-    alg = {"dek": per, "cid": per * (2 if ct is not None else 1)}
+    # algorithmic bytes = 1 B of HBM read per plaintext byte
+    # hashed; a launch of either pass covers `per` plaintext bytes.  The CID
+    # pass also writes the ctext (1 B/B more): that is in `traffic` (PMC) and
+    # kernel_traffic_frac, not in `achieved`.
+    alg = {"dek": per, "cid": per}
+    kern_bytes = {"dek": per, "cid": per * (2 if ct is not None else 1)}
     dom = max(avg, key=avg.get)
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
-    traffic = None
+    traffic, clock = None, {}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
-            t = json.load(open(tf)).get(dom, {})
+            pm = json.load(open(tf))
+            t = pm.get(dom, {})
             # profiled at the 64 GiB launch; traffic is linear in blocks
-            traffic = int(t["hbm_bytes_per_launch"] * alg[dom] / t["algorithmic_bytes"])
+            traffic = int(t["hbm_bytes_per_launch"] * kern_bytes[dom] / t["algorithmic_bytes"])
+            clock = pm.get("clock_GHz", {})
         except Exception:
             traffic = None
+    ms_step = step_ms if step_ms else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": {"dek": "k_pass<4,false,true,true> (keyed BLAKE3, DEK)",
                        "cid": "k_pass<4,true,true,true> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
             "algorithmic_bytes_per_launch": alg[dom],
+            "algorithmic_model": "SURVEY 8(d): 1 B of HBM read per plaintext byte hashed",
+            "kernel_traffic_frac": (round(traffic / (avg[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                    if traffic else None),
+            "step_frac": (round(total_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                          if ms_step else None),
             "avg_ms": {k: round(v, 4) for k, v in avg.items()},
             "hashed_GBps": {k: round(per / (v * 1e-3) / 1e9, 1) for k, v in avg.items()}}
     # ideal: each wave-cycle of a SIMD covers 64 lanes x 64 B blocks
@@ -275,6 +279,11 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5):
             "ideal_ms": {k: round(v, 3) for k, v in ideal_ms.items()},
             "achieved_ms": {k: round(v, 3) for k, v in avg.items()},
             "frac": {k: round(ideal_ms[k] / avg[k], 3) for k in avg},
+            "held_clock_GHz": {k: round(v, 3) for k, v in clock.items()},
+            "frac_at_held_clock": {k: round(ideal_ms[k] * PEAK_GHZ / clock[k] / avg[k], 3)
+                                   for k in avg if k in clock},
+            "held_clock_source": "GRBM_GUI_ACTIVE / 8 / duration, rocprofv3 PMC pass of the "
+                                 "same launches (profiles/pmc_traffic.json)",
             "instr_per_byte": INSTR_PER_BYTE}
     del refs
     roof["read_side"] = read

@@ -47,3 +47,32 @@ def root_from_level1(N, block_size: int, salt, cid_key, level1: bytes, size: int
     N.check(N.lib.glfsx_root_from_level1(block_size, salt, cid_key, level1,
                                          len(level1) // 64, size, ctypes.byref(r)))
     return bytes(r.ref)
+
+
+def write_sharded(N, dist, block_size: int, salt, cid_key, d_range: int, total: int,
+                  first_block: int, nb: int, d_ctext, stream):
+    """One rank's part of a sharded bigblob write, collective over
+    `dist` (a torch.distributed process group; gloo carries 64 B per bf
+    blocks): post this rank's blocks and level-1 nodes on its GPU, gather
+    every rank's level-1 refs, and on rank 0 build levels >= 2 and the root.
+    Returns (this rank's level-1 refs, the root ref on rank 0 else None).
+    A blob of at most bf blocks has no level >= 2: its single level-1 node is
+    posted by the rank that owns all of its blocks (rank 0)."""
+    import torch
+    rank, world = dist.get_rank(), dist.get_world_size()
+    mine = shard_device(N, block_size, salt, cid_key, d_range, total, first_block, nb,
+                        d_ctext, stream) if nb else b""
+    t = torch.frombuffer(bytearray(mine), dtype=torch.uint8) if mine else \
+        torch.zeros(0, dtype=torch.uint8)
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([t.numel()], dtype=torch.int64))
+    cap = max(1, int(max(x.item() for x in sizes)))
+    padded = torch.zeros(cap, dtype=torch.uint8)
+    padded[:t.numel()] = t
+    gathered = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(gathered, padded)   # the only exchange: 64 B per bf blocks
+    if rank != 0:
+        return mine, None
+    allrefs = b"".join(bytes(g[:int(k.item())].numpy().tobytes())
+                       for g, k in zip(gathered, sizes))
+    return mine, root_from_level1(N, block_size, salt, cid_key, allrefs, total)

@@ -1,9 +1,12 @@
 """Multi-rank sharding of one bigblob write, on CPU.
 
 glfs_amd.shard.plan partitions the blocks into bf-aligned ranges; each rank
-computes its level-1 refs (here with the oracle standing in for the GPU, test
-infrastructure only), the ranks all_gather them over gloo, and the root built
-from the gathered refs must equal the oracle's root of the whole blob.
+computes its level-1 refs (here, on CPU, with the oracle standing in for the
+GPU -- test infrastructure only), the ranks all_gather them over gloo, and the
+root built from the gathered refs must equal the oracle's root of the whole
+blob.  The same exchange with the product on the GPU (glfs_amd.shard.
+write_sharded in spawned rank processes, and bench.py's N>1 path under
+torch.distributed.run) is tests/test_gpu_shard_mp.py.
 """
 import os
 import random
