@@ -22,6 +22,8 @@ GLFSX_E_DEVICE = -4
 GLFSX_E_ARG = -5
 GLFSX_E_UNSUPPORTED = -6
 GLFSX_E_NOMEM = -7
+GLFSX_STORE_TRUST = 0
+GLFSX_STORE_HASH = 1
 
 
 class GlfsxError(RuntimeError):
@@ -92,12 +94,23 @@ SIGNATURES = {
     "glfsx_chacha20_xor": (_INT, [_CP, _VP, _VP, _U64]),
     "glfsx_fill_splitmix_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
     "glfsx_decrypt_batch_device": (_INT, [_VP, _U64, _U64, _VP, _VP, _VP]),
+    "glfsx_decrypt_batch": (_INT, [_VP, _U64, _U64, _VP, _VP]),
     "glfsx_sink_count": (_INT, [_VP, _INT, _VP, _VP, _U64]),
     "glfsx_tree_encode": (_INT, [_U64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _U64,
                                  ctypes.POINTER(ctypes.c_uint64), _VP]),
     "glfsx_tree_encode_device": (_INT, [_U64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                         _U64, _VP, ctypes.POINTER(ctypes.c_uint64), _VP]),
     "glfsx_fill_splitmix_blobs_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
+    "glfsx_store_new": (_VP, [_U64, _INT, _U64, _INT, _CP]),
+    "glfsx_store_free": (None, [_VP]),
+    "glfsx_store_post": (_INT, [_VP, _INT, _VP, _VP, _U64]),
+    "glfsx_store_exists": (_INT, [_VP, _CP]),
+    "glfsx_store_get": (_INT, [_VP, _CP, ctypes.POINTER(ctypes.c_void_p),
+                               ctypes.POINTER(ctypes.c_uint64)]),
+    "glfsx_store_stats": (_U64, [_VP, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64)]),
+    "glfsx_store_error": (_CP, [_VP]),
     "glfsx_depth": (_INT, [_U64, _U64]),
     "glfsx_branching_factor": (_U64, [_U64]),
 }

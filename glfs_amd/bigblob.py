@@ -94,8 +94,13 @@ def branching_factor(block_size: int) -> int:
 
 
 def _make_post_cb(store: Optional[WO]):
+    """(post function, error list, post_ctx) for the C-ABI.  A NativeStore
+    is passed as its C function (no Python per Post)."""
     if store is None:
-        return N.POST_FN(0), None
+        return N.POST_FN(0), None, None
+    native = getattr(store, "native_post", None)
+    if native is not None:
+        return native[0], [], native[1]
     errors: list = []
 
     def cb(_ctx, kind, ref, ctext, n):
@@ -107,7 +112,7 @@ def _make_post_cb(store: Optional[WO]):
             errors.append(e)
             return 1
 
-    return N.POST_FN(cb), errors
+    return N.POST_FN(cb), errors, None
 
 
 class Writer:
@@ -115,10 +120,10 @@ class Writer:
 
     def __init__(self, machine: "Machine", store: WO, salt: Optional[bytes],
                  cid_key: Optional[bytes] = None, strict: bool = False):
-        self._cb, self._errors = _make_post_cb(store)
+        self._cb, self._errors, ctx = _make_post_cb(store)
         err = ctypes.c_int(0)
         self._w = N.lib.glfsx_writer_new(machine.block_size, store.max_size(),
-                                         _salt_arg(salt), cid_key, self._cb, None,
+                                         _salt_arg(salt), cid_key, self._cb, ctx,
                                          ctypes.byref(err))
         if not self._w:
             N.check(err.value)
@@ -138,13 +143,18 @@ class Writer:
         if rc:
             self._raise(rc)
 
-    def write(self, data: bytes) -> int:
-        """blob.go:120-133."""
-        data = bytes(data)
-        rc = N.lib.glfsx_writer_write(self._w, data, len(data))
+    def write(self, data) -> int:
+        """blob.go:120-133 (any bytes-like object; not copied on the way)."""
+        if isinstance(data, bytes):
+            buf, n = data, len(data)
+        else:
+            mv = memoryview(data).cast("B")
+            n = len(mv)
+            buf = (ctypes.c_char * n).from_buffer(mv) if not mv.readonly else bytes(mv)
+        rc = N.lib.glfsx_writer_write(self._w, buf, n)
         if rc:
             self._raise(rc)
-        return len(data)
+        return n
 
     def finish(self) -> Root:
         """blob.go:135-150."""
@@ -264,25 +274,26 @@ class Machine:
 
     def sync(self, dst, src, x: Root, fn=None) -> None:
         """blob.go:270-315 Sync: nothing to do if dst has the root CID;
-        otherwise call fn(reader), then copy every reachable blob (children
-        before their index node)."""
+        otherwise call fn(reader), then copy every reachable blob, children
+        before their index node (the reference's post-order).  The index
+        levels are read one batched GPU decrypt per level."""
         if exists_unit(dst, x.ref.cid):
             return
         if fn is not None:
             fn(self.new_reader(src, x))
-        self._sync(dst, src, x.block_size, x.ref, depth(x.size, x.block_size))
+        levels = _tree_levels(src.get, x)
+        bf = branching_factor(x.block_size)
 
-    def _sync(self, dst, src, bs, ref: Ref, level: int) -> None:
-        if level > 0:
-            data = self.get_f(src, ref)
-            if len(data) != bs:
-                raise ValueError("data is not correct size for index")
-            for i in range(bs // MAX_REF_SIZE):
-                r2 = Ref.from_bytes(data[i * MAX_REF_SIZE:(i + 1) * MAX_REF_SIZE])
-                if r2.cid == bytes(CID_SIZE):
-                    break
-                self._sync(dst, src, bs, r2, level - 1)
-        copy_blob(dst, src, ref)
+        def emit(k: int, j: int) -> None:
+            if k + 1 < len(levels):
+                for c in range(j * bf, min((j + 1) * bf, len(levels[k + 1]))):
+                    emit(k + 1, c)
+            copy_blob(dst, src, levels[k][j])
+
+        if x.size == 0:
+            copy_blob(dst, src, x.ref)
+        else:
+            emit(0, 0)
 
     def populate(self, store, root: Root, dst) -> None:
         """blob.go:317-331 Populate: add every reachable CID that dst lacks
@@ -408,6 +419,64 @@ class ErrNotFound(KeyError):
         self.cid = cid
 
 
+class NativeStore:
+    """The native store of the C-ABI (glfsx_store_*, include/glfsx.h): an
+    in-memory content-addressed store whose Post takes the GPU-computed CID
+    (mode "trust": a pre-hashed Post; verify_every=k re-hashes every k-th
+    Post on the host) or re-hashes every ctext on the host as blobcache's
+    MemStore.Post does behind ref.go:103 (mode "hash").  The Writer hands it
+    its Posts as a C function pointer: no Python per Post."""
+
+    def __init__(self, max_size: int, mode: str = "trust", verify_every: int = 0,
+                 keep_data: bool = True, cid_key: Optional[bytes] = None):
+        m = {"trust": N.GLFSX_STORE_TRUST, "hash": N.GLFSX_STORE_HASH}[mode]
+        self._max = max_size
+        self._s = N.lib.glfsx_store_new(max_size, m, verify_every, int(keep_data), cid_key)
+        if not self._s:
+            raise N.GlfsxError(N.GLFSX_E_UNSUPPORTED,
+                               "host BLAKE3 (libclang-cpp.so) unavailable for a hashing store")
+        self.native_post = (ctypes.cast(N.lib.glfsx_store_post, N.POST_FN),
+                            ctypes.c_void_p(self._s))
+
+    def max_size(self) -> int:
+        return self._max
+
+    def post(self, ctext: bytes, ref: bytes, kind: int = KIND_DATA) -> None:
+        rc = N.lib.glfsx_store_post(self._s, kind, ref, ctext, len(ctext))
+        if rc:
+            raise StoreError(rc, (N.lib.glfsx_store_error(self._s) or b"").decode())
+
+    def exists(self, cid: bytes) -> bool:
+        return bool(N.lib.glfsx_store_exists(self._s, bytes(cid)))
+
+    def get(self, cid: bytes) -> bytes:
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        if N.lib.glfsx_store_get(self._s, bytes(cid), ctypes.byref(p), ctypes.byref(n)):
+            raise ErrNotFound(bytes(cid))
+        return ctypes.string_at(p, n.value) if n.value else b""
+
+    def stats(self) -> dict:
+        posts, nbytes, hashed = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        blobs = N.lib.glfsx_store_stats(self._s, ctypes.byref(posts), ctypes.byref(nbytes),
+                                        ctypes.byref(hashed))
+        return {"blobs": blobs, "posts": posts.value, "bytes": nbytes.value,
+                "rehashed": hashed.value}
+
+    def __len__(self) -> int:
+        return self.stats()["blobs"]
+
+    def close(self) -> None:
+        if self._s:
+            N.lib.glfsx_store_free(self._s)
+            self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class MemStore:
     """In-memory stand-in for blobcache's schema.MemStore [ext].  It keeps
     (CID -> ctext) as posted by the GPU path (a pre-hashed Post: the CID was
@@ -453,33 +522,73 @@ def crypto_xor(dek: bytes, data: bytes) -> bytes:
     return out.raw[:len(data)]
 
 
-def read_all(store: MemStore, root: Root) -> bytes:
-    """Read side (blob.go:31-69 ReadAt/getPiece, ref.go:113-126 getF) for
-    round-trip verification: walk the index tree, decrypt each blob."""
+def decrypt_level(ctexts, refs, block_size: int) -> list:
+    """getF (ref.go:113-126) for the blobs of one tree level at once: every
+    ctext but the last is exactly block_size bytes (index nodes; a blob's
+    data blocks), decrypted with its ref's DEK in ONE batched GPU call
+    (glfsx_decrypt_batch).  Returns the plaintexts in order."""
+    n = len(ctexts)
+    if n == 0:
+        return []
+    if any(len(c) != block_size for c in ctexts[:-1]) or len(ctexts[-1]) > block_size \
+            or block_size % 64:
+        return [crypto_xor(r.dek, c) for r, c in zip(refs, ctexts)]
+    data = b"".join(ctexts)
+    rb = b"".join(r.marshal_binary() for r in refs)
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    N.check(N.lib.glfsx_decrypt_batch(data, len(data), block_size, rb, out))
+    raw = out.raw
+    return [raw[i * block_size:i * block_size + len(c)] for i, c in enumerate(ctexts)]
+
+
+def _tree_levels(get, root: Root) -> list:
+    """The refs of every level of root's tree, top (the root) first, data
+    blocks last: each index level is fetched with get(cid) and decrypted in
+    one batch (blob.go:53-69 getPiece's walk, level by level)."""
     bs = root.block_size
     bf = branching_factor(bs)
     lvl = depth(root.size, bs)
+    n0 = -(-root.size // bs)
+    levels = [[root.ref]]
+    for k in range(lvl, 0, -1):
+        refs = levels[-1]
+        nodes = decrypt_level([get(r.cid) for r in refs], refs, bs)
+        want = -(-n0 // bf ** (k - 1))          # refs at level k-1
+        child = []
+        for node in nodes:
+            if len(node) != bf * MAX_REF_SIZE:
+                raise ValueError("data is not correct size for index")
+            take = min(bf, want - len(child))
+            child += [Ref.from_bytes(node[i * 64:(i + 1) * 64]) for i in range(take)]
+        levels.append(child)
+    return levels
 
-    def get_f(ref: Ref) -> bytes:
-        return crypto_xor(ref.dek, store.get(ref.cid))
 
-    out = io.BytesIO()
-
-    def walk(ref: Ref, level: int, remaining: int) -> int:
-        data = get_f(ref)
-        if level == 0:
-            out.write(data)
-            return len(data)
-        if len(data) != bf * MAX_REF_SIZE:
-            raise ValueError("data is not correct size for index")
-        got = 0
-        for i in range(bf):
-            if got >= remaining:
-                break
-            child = Ref.from_bytes(data[i * 64:(i + 1) * 64])
-            got += walk(child, level - 1, remaining - got)
-        return got
-
-    if root.size:
-        walk(root.ref, lvl, root.size)
-    return out.getvalue()
+def read_all(store, root: Root) -> bytes:
+    """Read side (blob.go:31-69 ReadAt/getPiece, ref.go:113-126 getF) of a
+    whole blob: the index levels and then all data blocks, each level one
+    batched GPU decrypt (the data level straight into the output buffer)."""
+    if root.size == 0:
+        return b""
+    bs = root.block_size
+    data_refs = _tree_levels(store.get, root)[-1]
+    ct = bytearray(root.size)
+    off = 0
+    for r in data_refs:
+        c = store.get(r.cid)
+        if off + len(c) > root.size or (len(c) != bs and off + len(c) != root.size):
+            raise ValueError("data block of the wrong size")
+        ct[off:off + len(c)] = c
+        off += len(c)
+    if off != root.size:
+        raise ValueError(f"blob read {off} bytes, root says {root.size}")
+    if bs % 64:
+        return b"".join(crypto_xor(r.dek, bytes(ct[i * bs:(i + 1) * bs]))
+                        for i, r in enumerate(data_refs))
+    out = bytearray(root.size)
+    rb = b"".join(r.marshal_binary() for r in data_refs)
+    cbuf = (ctypes.c_char * len(ct)).from_buffer(ct)
+    obuf = (ctypes.c_char * len(out)).from_buffer(out)
+    N.check(N.lib.glfsx_decrypt_batch(cbuf, len(ct), bs, rb, obuf))
+    del cbuf, obuf
+    return bytes(out)

@@ -1392,6 +1392,74 @@ int glfsx_fill_splitmix_blobs_device(void *d_dst, uint64_t n, uint64_t len,
   return 0;
 }
 
+// Batched getF decrypt from host memory: slabs of whole blocks through two
+// slots and three streams (upload k+1 / decrypt k / download k-1 overlap).
+int glfsx_decrypt_batch(const void *ctext, uint64_t total, uint64_t block_size,
+                        const uint8_t *refs, void *ptext) {
+  if (total == 0) return 0;
+  if (!ctext || !refs || !ptext) return fail(GLFSX_E_ARG, "null argument");
+  if (block_size == 0 || block_size % 64)
+    return fail(GLFSX_E_UNSUPPORTED, "decrypt needs block_size %% 64 == 0");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  const uint64_t n = (total + block_size - 1) / block_size;
+  const uint64_t slab_blocks = std::max<uint64_t>(1, (64ull << 20) / block_size);
+  struct Slot {
+    DevBuf d_in, d_out, d_refs;
+    PinBuf h_in, h_out;
+    hipEvent_t up = nullptr, done = nullptr;
+    uint64_t b0 = 0, nb = 0, bytes = 0;
+    bool busy = false;
+  };
+  static thread_local Slot slots[2];
+  static thread_local hipStream_t s_up = nullptr, s_dn = nullptr;
+  if (!s_up) {
+    HIP_TRY(hipStreamCreateWithFlags(&s_up, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&s_dn, hipStreamNonBlocking));
+  }
+  auto finish = [&](Slot &sl) -> int {
+    if (!sl.busy) return 0;
+    sl.busy = false;
+    HIP_TRY(hipEventSynchronize(sl.done));
+    par_memcpy(static_cast<uint8_t *>(ptext) + sl.b0 * block_size, sl.h_out.u8(), sl.bytes);
+    return 0;
+  };
+  int k = 0;
+  for (uint64_t b0 = 0; b0 < n; b0 += slab_blocks, k ^= 1) {
+    Slot &sl = slots[k];
+    if (int e = finish(sl)) return e;
+    sl.b0 = b0;
+    sl.nb = std::min(slab_blocks, n - b0);
+    sl.bytes = std::min<uint64_t>(sl.nb * block_size, total - b0 * block_size);
+    if (int e = sl.d_in.ensure(sl.bytes + 64)) return e;
+    if (int e = sl.d_out.ensure(sl.bytes + 64)) return e;
+    if (int e = sl.d_refs.ensure(64 * sl.nb)) return e;
+    if (int e = sl.h_in.ensure(sl.bytes + 64 * sl.nb)) return e;
+    if (int e = sl.h_out.ensure(sl.bytes)) return e;
+    if (!sl.up) {
+      HIP_TRY(hipEventCreateWithFlags(&sl.up, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    par_memcpy(sl.h_in.u8(), static_cast<const uint8_t *>(ctext) + b0 * block_size, sl.bytes);
+    memcpy(sl.h_in.u8() + sl.bytes, refs + 64 * b0, 64 * sl.nb);
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, sl.bytes, hipMemcpyHostToDevice, s_up));
+    HIP_TRY(hipMemcpyAsync(sl.d_refs.p, sl.h_in.u8() + sl.bytes, 64 * sl.nb,
+                           hipMemcpyHostToDevice, s_up));
+    HIP_TRY(hipEventRecord(sl.up, s_up));
+    HIP_TRY(hipStreamWaitEvent(c->stream, sl.up, 0));
+    HIP_TRY(launch_decrypt(sl.d_in.u8(), sl.d_out.u8(), sl.nb, block_size,
+                           sl.bytes - (sl.nb - 1) * block_size, sl.d_refs.u8(), c->stream));
+    HIP_TRY(hipEventRecord(sl.up, c->stream));
+    HIP_TRY(hipStreamWaitEvent(s_dn, sl.up, 0));
+    HIP_TRY(hipMemcpyAsync(sl.h_out.p, sl.d_out.p, sl.bytes, hipMemcpyDeviceToHost, s_dn));
+    HIP_TRY(hipEventRecord(sl.done, s_dn));
+    sl.busy = true;
+  }
+  for (int i = 0; i < 2; ++i, k ^= 1)
+    if (int e = finish(slots[k])) return e;
+  return 0;
+}
+
 // A store sink that only counts (benchmarks, tests): ctx -> uint64_t[2] =
 // {posts, bytes}.  Stands in for a native store's Post at ~zero cost.
 int glfsx_sink_count(void *ctx, int kind, const uint8_t *ref, const void *ctext,

@@ -114,10 +114,10 @@ class Machine:
         O = (ctypes.c_uint64 * n)(*offs)
         L = (ctypes.c_uint64 * n)(*lens)
         roots = ctypes.create_string_buffer(64 * n)
-        cb, errors = bigblob._make_post_cb(store)
+        cb, errors, ctx = bigblob._make_post_cb(store)
         rc = N.lib.glfsx_post_blobs(self.block_size, store.max_size(),
                                     self.make_salt(TYPE_BLOB), None, data or b"\0",
-                                    O, L, n, cb, None, roots)
+                                    O, L, n, cb, ctx, roots)
         if rc == N.GLFSX_E_STORE and errors:
             raise bigblob.StoreError(rc, repr(errors[0])) from errors[0]
         N.check(rc)

@@ -26,6 +26,8 @@
  *                          single-block blobs (tree.go:300-316 callers)
  *   glfsx_depth            bigblob/blob.go:256-264 depth()
  *   glfsx_tree_encode      tree.go:300-316 TreeWriter.Put's JSON lines, batched
+ *   glfsx_store_*          the store under ref.go:103 (bcsdk.WO / MemStore [ext])
+ *                          with a pre-hashed Post that takes the GPU CID
  *   glfsx_chacha20_xor*    bigblob/ref.go:137-144  cryptoXOR (read side decrypt)
  *
  * Conventions:
@@ -284,6 +286,44 @@ int glfsx_sink_count(void *ctx, int kind, const uint8_t *ref, const void *ctext,
 int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
                                uint64_t block_size, const void *d_refs,
                                void *d_ptext, void *stream);
+
+/* --- store boundary (bcsdk.WO [ext], ref.go:103) ----- */
+/* An in-memory content-addressed store in blobcache MemStore's role (CID ->
+ * ctext, MaxSize, Get, Exists) whose Post takes the GPU-computed CID.
+ *   GLFSX_STORE_TRUST: a pre-hashed Post -- no host hashing; verify_every =
+ *     k > 0 re-hashes every k-th Post on the host (parity mode) and fails it
+ *     on a mismatch;
+ *   GLFSX_STORE_HASH: every Post re-hashes the ctext on the calling thread,
+ *     as MemStore.Post does behind ref.go:103 (today's cost of the drop-in),
+ *     failing on a mismatch.
+ * The host hash is the image's upstream BLAKE3 C (libclang-cpp.so); without
+ * it the hashing modes return NULL.  keep_data 0 keeps CIDs and lengths
+ * only.  cid_key: the store's BLAKE3 key (NULL = unkeyed, as glfsx's CID).
+ * glfsx_store_post is a glfsx_post_fn: pass it with the store as post_ctx. */
+typedef struct glfsx_store glfsx_store;
+enum { GLFSX_STORE_TRUST = 0, GLFSX_STORE_HASH = 1 };
+glfsx_store *glfsx_store_new(uint64_t max_size, int mode, uint64_t verify_every,
+                             int keep_data, const uint8_t *cid_key);
+void glfsx_store_free(glfsx_store *s);
+int glfsx_store_post(void *store, int kind, const uint8_t *ref, const void *ctext,
+                     uint64_t len);
+int glfsx_store_exists(glfsx_store *s, const uint8_t cid[32]);
+/* GLFSX_E_STORE when absent (blobcache.ErrNotFound); *data stays valid
+ * until the store is freed. */
+int glfsx_store_get(glfsx_store *s, const uint8_t cid[32], const void **data,
+                    uint64_t *len);
+/* number of distinct blobs; posts, bytes posted, posts re-hashed */
+uint64_t glfsx_store_stats(glfsx_store *s, uint64_t *posts, uint64_t *bytes,
+                           uint64_t *hashed);
+const char *glfsx_store_error(glfsx_store *s);
+
+/* Batched getF decrypt from host memory (ref.go:113-126 over a tree level:
+ * index nodes, or a blob's data blocks): block j of ctext (block_size bytes,
+ * the last one short; block_size % 64 == 0) decrypted with the DEK in bytes
+ * [32,64) of the 64-byte ref j of refs (host) into ptext (host).  Uploads,
+ * decrypts and downloads overlap in 64 MiB slabs. */
+int glfsx_decrypt_batch(const void *ctext, uint64_t total, uint64_t block_size,
+                        const uint8_t *refs, void *ptext);
 
 /* --- tree shape (blob.go:219-268) -------------------------------------- */
 int glfsx_depth(uint64_t size, uint64_t block_size);
