@@ -133,6 +133,8 @@ except ImportError:  # a plain C consumer (e.g. a cgo binding) needs no torch
 
 lib = ctypes.CDLL(LIB_PATH)
 for _name, (_res, _args) in SIGNATURES.items():
+    if os.environ.get("GLFSX_LIB") and not hasattr(lib, _name):
+        continue  # an older build under A/B comparison
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args

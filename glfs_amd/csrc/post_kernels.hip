@@ -147,9 +147,95 @@ __device__ __forceinline__ uint32_t add3_a(uint32_t a, uint32_t b, uint32_t c) {
 #define B3G(a, b, c, d, x, y) B3G_C(a, b, c, d, x, y)
 #endif
 
+// GLFSX_SCHED: the ARX rounds of the many-wave kernels written step by step
+// over all independent chains of a half-round (4 G or 4 QR; 8 when a BLAKE3
+// round is fused with a ChaCha20 double round), with a scheduling barrier
+// after each step, so the compiler cannot serialise the chains: two
+// dependent instructions are always at least 3 (7 fused) independent ones
+// apart.  1 = compiler-visible C form (no hazard nops), 2 = the one-asm-
+// statement-per-instruction form (default: measured +2.5% config 2, +1-2%
+// small blobs and read side, headline unchanged; 1 was 5.7% slower).  0 =
+// the plain macros above.
+#ifndef GLFSX_SCHED
+#define GLFSX_SCHED 2
+#endif
+#define SB() __builtin_amdgcn_sched_barrier(0)
+constexpr int kCol[4][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}};
+constexpr int kDia[4][4] = {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
+
+template <int F>
+__device__ __forceinline__ uint32_t s_add(uint32_t a, uint32_t b) {
+  if constexpr (F == 2) return add_a(a, b); else return a + b;
+}
+template <int F>
+__device__ __forceinline__ uint32_t s_add3(uint32_t a, uint32_t b, uint32_t c) {
+  if constexpr (F == 2) return add3_a(a, b, c); else return a + b + c;
+}
+template <int F>
+__device__ __forceinline__ uint32_t s_xor(uint32_t a, uint32_t b) {
+  if constexpr (F == 2) return xor_a(a, b); else return a ^ b;
+}
+template <int F, int N>
+__device__ __forceinline__ uint32_t s_rot(uint32_t x) {
+  if constexpr (F == 2) return rotr_a<N>(x); else return rotr(x, N);
+}
+
+// One half-round, 12 steps: B3 (if G) = 4 BLAKE3 G's on v with message words
+// m[s[mo + 2k]], m[s[mo + 2k + 1]]; Q (if Q) = 4 ChaCha20 quarter-rounds on x.
+template <int F, bool DIAG, int R, bool G, bool Q>
+__device__ __forceinline__ void half_il(uint32_t (&v)[16], const uint32_t (&m)[16],
+                                        uint32_t (&x)[16]) {
+  constexpr const int (*I)[4] = DIAG ? kDia : kCol;
+  constexpr const int *s = kSched.s[R];
+  constexpr int mo = DIAG ? 8 : 0;
+#define IL_STEP(gstmt, qstmt)                        \
+  _Pragma("unroll") for (int k = 0; k < 4; ++k) {    \
+    if constexpr (G) { gstmt; }                      \
+    if constexpr (Q) { qstmt; }                      \
+  }                                                  \
+  SB();
+#define VA v[I[k][0]]
+#define VB v[I[k][1]]
+#define VC v[I[k][2]]
+#define VD v[I[k][3]]
+#define XA x[I[k][0]]
+#define XB x[I[k][1]]
+#define XC x[I[k][2]]
+#define XD x[I[k][3]]
+  IL_STEP(VA = s_add3<F>(VA, VB, m[s[mo + 2 * k]]), XA = s_add<F>(XA, XB))
+  IL_STEP(VD = s_xor<F>(VD, VA), XD = s_xor<F>(XD, XA))
+  IL_STEP(VD = (s_rot<F, 16>(VD)), XD = (s_rot<F, 16>(XD)))
+  IL_STEP(VC = s_add<F>(VC, VD), XC = s_add<F>(XC, XD))
+  IL_STEP(VB = s_xor<F>(VB, VC), XB = s_xor<F>(XB, XC))
+  IL_STEP(VB = (s_rot<F, 12>(VB)), XB = (s_rot<F, 20>(XB)))
+  IL_STEP(VA = s_add3<F>(VA, VB, m[s[mo + 2 * k + 1]]), XA = s_add<F>(XA, XB))
+  IL_STEP(VD = s_xor<F>(VD, VA), XD = s_xor<F>(XD, XA))
+  IL_STEP(VD = (s_rot<F, 8>(VD)), XD = (s_rot<F, 24>(XD)))
+  IL_STEP(VC = s_add<F>(VC, VD), XC = s_add<F>(XC, XD))
+  IL_STEP(VB = s_xor<F>(VB, VC), XB = s_xor<F>(XB, XC))
+  IL_STEP(VB = (s_rot<F, 7>(VB)), XB = (s_rot<F, 25>(XB)))
+#undef VA
+#undef VB
+#undef VC
+#undef VD
+#undef XA
+#undef XB
+#undef XC
+#undef XD
+#undef IL_STEP
+}
+
 template <int R, bool A = true>
 __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
                                          const uint32_t (&m)[16]) {
+#if GLFSX_SCHED
+  if constexpr (A && R > 0) {
+    uint32_t x[16];
+    half_il<GLFSX_SCHED, false, R, true, false>(v, m, x);
+    half_il<GLFSX_SCHED, true, R, true, false>(v, m, x);
+    return;
+  }
+#endif
   constexpr const int *s = kSched.s[R];
   B3G(v[0], v[4], v[8], v[12], m[s[0]], m[s[1]]);
   B3G(v[1], v[5], v[9], v[13], m[s[2]], m[s[3]]);
@@ -221,6 +307,14 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
   CQR(x[3], x[4], x[9], x[14]);
 #pragma unroll
   for (int i = 1; i < 10; ++i) {
+#if GLFSX_SCHED
+   if constexpr (A) {
+    uint32_t v[16], m[16];
+    half_il<GLFSX_SCHED, false, 0, false, true>(v, m, x);
+    half_il<GLFSX_SCHED, true, 0, false, true>(v, m, x);
+    continue;
+   }
+#endif
 #if GLFSX_ASM_ARX
    if constexpr (A) {
     CQR_A(x[0], x[4], x[8], x[12]);
@@ -337,22 +431,34 @@ struct KArgs {
   uint32_t *cnt;
 };
 
-// Split mode: publish this workgroup's subtree CV (thread 0 stored it to
-// scratch) and count it in; true in every thread of the workgroup that
-// arrives last for its message, which then merges all W CVs.  Agent-scope
-// release / acquire: the workgroups of one message run on different XCDs,
-// whose L2s are not coherent with each other without them.
+// Split mode: thread 0 publishes this workgroup's subtree CV and counts it
+// in; returns true in every thread of the workgroup that arrives last for
+// its message, which then merges all W CVs.  The workgroups of a message
+// run on different XCDs, whose L2s are not coherent with each other.  An
+// agent-scope release fence would write back the whole L2 of the issuing
+// XCD per workgroup (measured: +50 us per 1 GiB split pass); instead the CV
+// words are agent-scope atomic stores (written through to the coherence
+// point), the wave waits for them to complete, and only then increments the
+// counter (an agent-scope atomic, performed device-wide); the last
+// workgroup reads the CVs with agent-scope atomic loads.
+__device__ __forceinline__ void publish_cv(uint32_t *dst, const uint32_t (&cv)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    __hip_atomic_store(dst + i, cv[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t load_cv_word(const uint32_t *src) {
+  return __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ bool arrive_last(uint32_t *cnt, uint32_t W,
                                             uint32_t t, uint32_t *flag) {
   if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL,
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the CV stores are done
+    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
     *flag = old + 1 == W;
   }
   __syncthreads();
-  const bool last = *flag != 0;
-  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return last;
+  return *flag != 0;
 }
 
 // Merge step after the last block of local chunk jj: pop/parent/push on the
@@ -537,6 +643,17 @@ __device__ __forceinline__ void pair_pipelined(
   uint32_t v[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
                     kIV[0], kIV[1], kIV[2], kIV[3], chunk, 0u, 64u, fla};
   b3_round<0, true>(v, m);
+#if GLFSX_SCHED
+#define GQ_IL(R)                                           \
+  half_il<GLFSX_SCHED, false, R, true, true>(v, m, x);     \
+  half_il<GLFSX_SCHED, true, R, true, true>(v, m, x);
+  GQ_IL(1) GQ_IL(2) GQ_IL(3) GQ_IL(4) GQ_IL(5) GQ_IL(6)
+#undef GQ_IL
+  for (int i = 0; i < 3; ++i) {
+    half_il<GLFSX_SCHED, false, 0, false, true>(v, m, x);
+    half_il<GLFSX_SCHED, true, 0, false, true>(v, m, x);
+  }
+#else
   gq_round<1>(v, m, x);
   gq_round<2>(v, m, x);
   gq_round<3>(v, m, x);
@@ -546,6 +663,7 @@ __device__ __forceinline__ void pair_pipelined(
   CDR_A(x);
   CDR_A(x);
   CDR_A(x);
+#endif
 #pragma unroll
   for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
   x[0] += c0;
@@ -890,21 +1008,16 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   // last workgroup merges the W = ceil(len / span) CVs (left-complete tree,
   // ROOT on the last parent) and resets the counter for the next launch
   const uint64_t wbase = j << a.split_log2;
-  if (t == 0) {
-    uint4 *q = reinterpret_cast<uint4 *>(a.scratch + (wbase + sidx) * 8);
-    q[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
-    q[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
-  }
+  if (t == 0) publish_cv(a.scratch + (wbase + sidx) * 8, cv);
   const uint32_t W = uint32_t((len_full + kSpan - 1) / kSpan);
   __shared__ uint32_t s_flag;
   if (!arrive_last(a.cnt + j, W, t, &s_flag)) return;
   if (t < W) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(a.scratch + (wbase + t) * 8);
-    const uint4 x = q[0], y = q[1];
-    cv[0] = x.x; cv[1] = x.y; cv[2] = x.z; cv[3] = x.w;
-    cv[4] = y.x; cv[5] = y.y; cv[6] = y.z; cv[7] = y.w;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
+    for (int i = 0; i < 8; ++i) {
+      cv[i] = load_cv_word(a.scratch + (wbase + t) * 8 + i);
+      lds[t * 8 + i] = cv[i];
+    }
   }
   __syncthreads();
   tree_reduce(lds, W, t, key, a.base, true, cv);
@@ -1099,18 +1212,14 @@ __global__ __launch_bounds__(1024) void k_quad(KArgs a) {
       w[k] = __builtin_amdgcn_readlane(cl, k);
       w[4 + k] = __builtin_amdgcn_readlane(ch, k);
     }
-    if (tid == 0) {
-      uint4 *p = reinterpret_cast<uint4 *>(a.scratch + (wbase + sidx) * 8);
-      p[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      p[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    }
+    if (tid == 0) publish_cv(a.scratch + (wbase + sidx) * 8, w);
   }
   const uint32_t W = uint32_t((len + kSpan - 1) / kSpan);
   __shared__ uint32_t s_flag;
   if (!arrive_last(a.cnt + j, W, tid, &s_flag)) return;
   if (quad < W) {
-    cl = a.scratch[(wbase + quad) * 8 + q];
-    ch = a.scratch[(wbase + quad) * 8 + 4 + q];
+    cl = load_cv_word(a.scratch + (wbase + quad) * 8 + q);
+    ch = load_cv_word(a.scratch + (wbase + quad) * 8 + 4 + q);
   }
   count = W;
   while (count > 1) {  // uniform
