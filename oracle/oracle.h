@@ -100,6 +100,13 @@ void oracle_post_batch(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
                        const uint8_t *ptext, uint64_t total, uint64_t chunk,
                        const uint8_t *cid_key, int threads);
 
+/* The same post batch on the image's SIMD libraries (upstream BLAKE3 C with
+ * AVX-512 from libclang-cpp.so, OpenSSL ChaCha20), cpu_simd.c: a second
+ * CPU baseline for bench.py.  Returns -1 when a library is missing. */
+int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
+                           const uint8_t *ptext, uint64_t total, uint64_t chunk,
+                           const uint8_t *cid_key, int threads);
+
 /* Deterministic data generator shared by tests/bench: byte offset o ->
  * byte (o & 7) of splitmix64(seed ^ (o >> 3)), little-endian. */
 void oracle_fill_splitmix(uint8_t *dst, uint64_t offset, uint64_t n,

@@ -148,3 +148,21 @@ def test_write_granularity_invariance(O):
         got = O.create(data, 1024, salt=None, chunks=pieces)
         assert got[0] == want[0]
         assert [(p[0], p[1]) for p in got[3]] == [(p[0], p[1]) for p in want[3]]
+
+
+def test_simd_cpu_baseline_same_refs(O):
+    """bench's second CPU baseline (upstream BLAKE3 C + OpenSSL ChaCha20,
+    oracle/cpu_simd.c) computes the same refs and ctext as the scalar port."""
+    import ctypes
+    L = O.lib()
+    n, bs = 5 * 1024 * 1024 + 777, 1 << 20
+    data = O.fill_splitmix(n, 4)
+    salt = O.derive_key(bytes(32), b"raw")
+    nb = -(-n // bs)
+    a, b = ctypes.create_string_buffer(64 * nb), ctypes.create_string_buffer(64 * nb)
+    ca, cb = ctypes.create_string_buffer(n), ctypes.create_string_buffer(n)
+    L.oracle_post_batch(a, ca, salt, data, n, bs, None, 2)
+    rc = L.oracle_post_batch_simd(b, cb, salt, data, n, bs, None, 3)
+    if rc == -1:
+        pytest.skip("libclang-cpp BLAKE3 or libcrypto absent")
+    assert a.raw == b.raw and ca.raw == cb.raw
