@@ -137,6 +137,31 @@ class Writer:
             raise StoreError(rc, repr(self._errors[0])) from self._errors[0]
         N.check(rc, (N.lib.glfsx_writer_error(self._w) or b"").decode(errors="replace"))
 
+    def write_device(self, d_ptr: int, n: int, stream=None) -> int:
+        """Write n bytes already in HBM (device pointer), ordered after the
+        work on `stream` (a hipStream_t handle or None)."""
+        rc = N.lib.glfsx_writer_write_device(self._w, d_ptr, n, stream)
+        if rc:
+            self._raise(rc)
+        return n
+
+    def write_ctext(self, ctext, refs: bytes, block_size: int) -> int:
+        """Write the plaintext of data blocks given as ciphertext (decrypted
+        on the GPU with each ref's DEK; the plaintext never leaves the
+        device).  ctext: block j at j*block_size, the last block short."""
+        if hasattr(ctext, "ctypes"):   # a numpy array: pass its memory as is
+            buf, n = ctext.ctypes.data, ctext.nbytes
+        elif isinstance(ctext, bytes):
+            buf, n = ctext, len(ctext)
+        else:
+            mv = memoryview(ctext).cast("B")
+            n = len(mv)
+            buf = (ctypes.c_char * n).from_buffer(mv) if not mv.readonly else bytes(mv)
+        rc = N.lib.glfsx_writer_write_ctext(self._w, buf, n, block_size, bytes(refs))
+        if rc:
+            self._raise(rc)
+        return n
+
     def flush(self) -> None:
         """Deliver the Posts of every complete block written so far."""
         rc = N.lib.glfsx_writer_flush(self._w)
@@ -334,15 +359,46 @@ class Machine:
             w.close()
 
 
+def _gather(store, refs, size: int):
+    """The blobs of `refs`, concatenated into one uninitialised buffer of
+    `size` bytes (straight from a NativeStore's memory when possible)."""
+    import numpy as np
+    out = np.empty(size, dtype=np.uint8)
+    base, off = out.ctypes.data, 0
+    direct = hasattr(store, "get_into")
+    for ref in refs:
+        if direct:
+            off += store.get_into(ref.cid, base + off, size - off)
+        else:
+            c = store.get(ref.cid)
+            if off + len(c) > size:
+                raise ValueError("blob larger than its root says")
+            out[off:off + len(c)] = np.frombuffer(c, dtype=np.uint8)
+            off += len(c)
+    if off != size:
+        raise ValueError(f"blob read {off} bytes, root says {size}")
+    return out
+
+
 def _concat(machine: "Machine", store, block_size: int, salt, roots, cid_key=None) -> Root:
-    """blob.go:333-345 Concat: read every root (GPU decrypt of each blob via
-    the read side), stream the bytes through a new Writer.  Like the
-    reference, the `block_size` argument is ignored: the writer uses the
-    machine's block size (quirk recorded in SURVEY's appendix)."""
+    """blob.go:333-345 Concat: every root's bytes, in order, through a new
+    Writer.  The index levels are read with one batched decrypt per level;
+    the data blocks go to the Writer as ciphertext and are decrypted on the
+    GPU right into its staging (glfsx_writer_write_ctext), so the plaintext
+    never crosses PCIe.  Like the reference, the `block_size` argument is
+    ignored: the writer uses the machine's block size (quirk recorded in
+    SURVEY's appendix)."""
     w = machine.new_writer(store, salt, cid_key)
     try:
         for r in roots:
-            w.write(read_all(store, r))
+            if r.size == 0:
+                continue
+            data_refs = _tree_levels(store.get, r)[-1]
+            if r.block_size % 64:
+                w.write(read_all(store, r))
+                continue
+            ct = _gather(store, data_refs, r.size)
+            w.write_ctext(ct, b"".join(x.marshal_binary() for x in data_refs), r.block_size)
         return w.finish()
     finally:
         w.close()
@@ -454,6 +510,18 @@ class NativeStore:
         if N.lib.glfsx_store_get(self._s, bytes(cid), ctypes.byref(p), ctypes.byref(n)):
             raise ErrNotFound(bytes(cid))
         return ctypes.string_at(p, n.value) if n.value else b""
+
+    def get_into(self, cid: bytes, dst_addr: int, cap: int) -> int:
+        """Copy the blob straight from the store's memory to dst_addr (at
+        most cap bytes); returns its length."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        if N.lib.glfsx_store_get(self._s, bytes(cid), ctypes.byref(p), ctypes.byref(n)):
+            raise ErrNotFound(bytes(cid))
+        if n.value > cap:
+            raise ValueError("blob larger than the destination")
+        if n.value:
+            ctypes.memmove(dst_addr, p, n.value)
+        return n.value
 
     def stats(self) -> dict:
         posts, nbytes, hashed = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
@@ -572,23 +640,12 @@ def read_all(store, root: Root) -> bytes:
         return b""
     bs = root.block_size
     data_refs = _tree_levels(store.get, root)[-1]
-    ct = bytearray(root.size)
-    off = 0
-    for r in data_refs:
-        c = store.get(r.cid)
-        if off + len(c) > root.size or (len(c) != bs and off + len(c) != root.size):
-            raise ValueError("data block of the wrong size")
-        ct[off:off + len(c)] = c
-        off += len(c)
-    if off != root.size:
-        raise ValueError(f"blob read {off} bytes, root says {root.size}")
     if bs % 64:
-        return b"".join(crypto_xor(r.dek, bytes(ct[i * bs:(i + 1) * bs]))
-                        for i, r in enumerate(data_refs))
+        return b"".join(crypto_xor(r.dek, store.get(r.cid)) for r in data_refs)
+    ct = _gather(store, data_refs, root.size)
     out = bytearray(root.size)
     rb = b"".join(r.marshal_binary() for r in data_refs)
-    cbuf = (ctypes.c_char * len(ct)).from_buffer(ct)
     obuf = (ctypes.c_char * len(out)).from_buffer(out)
-    N.check(N.lib.glfsx_decrypt_batch(cbuf, len(ct), bs, rb, obuf))
-    del cbuf, obuf
+    N.check(N.lib.glfsx_decrypt_batch(ct.ctypes.data, len(ct), bs, rb, obuf))
+    del obuf
     return bytes(out)

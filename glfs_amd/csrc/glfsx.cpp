@@ -313,6 +313,8 @@ struct WSlot {
   uint64_t nblk = 0;  // blocks in flight
   uint64_t seq = 0;   // submission order
   bool busy = false;
+  bool on_dev = false;  // the staged bytes [0, used) live in d_in, not h_in
+                        // (written by glfsx_writer_write_device)
   int dev = -1;       // device of d_* (pool key)
 };
 
@@ -372,6 +374,11 @@ struct glfsx_writer {
   std::vector<uint64_t> counts;
   uint64_t size = 0;
   OneBuf one;                // single posts (index nodes, the tail block)
+  // device input (write_device / write_ctext): events ordering the caller's
+  // stream with the upload stream, and write_ctext's staging / temporaries
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  PinBuf h_ctx;
+  DevBuf d_ctx, d_ptx, d_rfx;
   WSlot slot[kMaxSlots];
   int nslots = 3;
   int cur = 0;               // slot being filled
@@ -430,17 +437,22 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
 // Post one message from host memory (ref.go:98 post + sink), synchronously,
 // on the writer's hash stream with the writer's own staging.
 int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
-             const uint8_t *data, uint64_t n, uint8_t ref[64]) {
+             const uint8_t *data, uint64_t n, uint8_t ref[64],
+             bool dev_src = false) {
   OneBuf &o = w->one;
   if (int e = o.d_in.ensure(n + 64)) return e;
   if (int e = o.d_ct.ensure(n + 64)) return e;
   if (int e = o.d_ref.ensure(64)) return e;
   if (int e = o.h_ct.ensure(n + 64)) return e;
   if (int e = o.h_ref.ensure(64)) return e;
-  if (n)
+  if (dev_src) {  // data is device memory written on the upload stream
+    HIP_TRY(hipEventRecord(w->ev_out, w->s_up));
+    HIP_TRY(hipStreamWaitEvent(w->ws, w->ev_out, 0));
+  } else if (n) {
     HIP_TRY(hipMemcpyAsync(o.d_in.p, data, n, hipMemcpyHostToDevice, w->ws));
+  }
   PostJob j{};
-  j.src = o.d_in.u8();
+  j.src = dev_src ? data : o.d_in.u8();
   j.ctext = o.d_ct.u8();
   j.stride = 0;
   j.msg_len = n;
@@ -517,7 +529,8 @@ int submit(glfsx_writer *w) {
     HIP_TRY(hipEventCreateWithFlags(&sl.hashed, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
   }
-  HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->s_up));
+  if (!sl.on_dev)  // device-written bytes are already in d_in (s_up order)
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->s_up));
   HIP_TRY(hipEventRecord(sl.up, w->s_up));
   HIP_TRY(hipStreamWaitEvent(w->ws, sl.up, 0));
   PostJob j{};
@@ -545,10 +558,64 @@ int submit(glfsx_writer *w) {
   // `nx` is the oldest batch in flight (submitted nslots-1 batches ago):
   // completing it keeps Posts in order
   if (int e = complete(w, nx)) return e;
-  if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
-  if (w->partial) memcpy(nx.h_in.u8(), sl.h_in.u8() + nbytes, w->partial);
+  if (sl.on_dev) {  // carry the partial block over on the device
+    if (int e = nx.d_in.ensure(w->batch_blocks * w->bs + 64)) return e;
+    if (w->partial)
+      HIP_TRY(hipMemcpyAsync(nx.d_in.p, sl.d_in.u8() + nbytes, w->partial,
+                             hipMemcpyDeviceToDevice, w->s_up));
+    nx.on_dev = true;
+  } else {
+    if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
+    if (w->partial) memcpy(nx.h_in.u8(), sl.h_in.u8() + nbytes, w->partial);
+    nx.on_dev = false;
+  }
   w->cur = next;
   w->full = 0;
+  return 0;
+}
+
+// Move the current slot's staged bytes between host and device staging.
+int slot_to_device(glfsx_writer *w) {
+  WSlot &sl = w->slot[w->cur];
+  if (sl.on_dev) return 0;
+  const uint64_t used = w->full * w->bs + w->partial;
+  if (int e = sl.d_in.ensure(w->batch_blocks * w->bs + 64)) return e;
+  if (used)
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, used, hipMemcpyHostToDevice, w->s_up));
+  sl.on_dev = true;
+  return 0;
+}
+
+int slot_to_host(glfsx_writer *w) {
+  WSlot &sl = w->slot[w->cur];
+  if (!sl.on_dev) return 0;
+  const uint64_t used = w->full * w->bs + w->partial;
+  if (int e = pin_grow(sl.h_in, std::max<uint64_t>(used, 1), 0)) return e;
+  if (used) {
+    HIP_TRY(hipMemcpyAsync(sl.h_in.p, sl.d_in.p, used, hipMemcpyDeviceToHost, w->s_up));
+    HIP_TRY(hipStreamSynchronize(w->s_up));
+  }
+  sl.on_dev = false;
+  return 0;
+}
+
+// Append n device bytes, ordered after everything already on the upload
+// stream (blob.go:120-133 block bookkeeping, as glfsx_writer_write).
+int write_dev(glfsx_writer *w, const uint8_t *p, uint64_t n) {
+  while (n) {
+    if (int e = slot_to_device(w)) return e;
+    WSlot &sl = w->slot[w->cur];
+    const uint64_t used = w->full * w->bs + w->partial;
+    const uint64_t cap = w->batch_blocks * w->bs;
+    const uint64_t take = std::min<uint64_t>(cap - used, n);
+    HIP_TRY(hipMemcpyAsync(sl.d_in.u8() + used, p, take, hipMemcpyDeviceToDevice, w->s_up));
+    p += take;
+    n -= take;
+    w->full = (used + take) / w->bs;
+    w->partial = (used + take) % w->bs;
+    if (w->full == w->batch_blocks)
+      if (int e = submit(w)) return e;
+  }
   return 0;
 }
 
@@ -876,6 +943,7 @@ int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
   if (n && !data) return call.done(fail(GLFSX_E_ARG, "null data"));
   const uint8_t *p = static_cast<const uint8_t *>(data);
   while (n) {
+    if (int e = slot_to_host(w)) return call.done(w->sticky = e);
     WSlot &sl = w->slot[w->cur];
     const uint64_t used = w->full * w->bs + w->partial;
     const uint64_t cap = w->batch_blocks * w->bs;  // slot holds up to a batch
@@ -902,6 +970,82 @@ int glfsx_writer_flush(glfsx_writer *w) {
   return 0;
 }
 
+int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
+                              void *stream) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (n && !d_data) return call.done(fail(GLFSX_E_ARG, "null data"));
+  if (n == 0) return 0;
+  hipStream_t cs = static_cast<hipStream_t>(stream);
+  auto go = [&]() -> int {
+    if (!w->ev_in) {
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
+    }
+    if (cs) {  // the bytes are ready once the caller's stream gets here
+      HIP_TRY(hipEventRecord(w->ev_in, cs));
+      HIP_TRY(hipStreamWaitEvent(w->s_up, w->ev_in, 0));
+    }
+    if (int e = write_dev(w, static_cast<const uint8_t *>(d_data), n)) return e;
+    // the caller may reuse d_data once its stream passes this point
+    HIP_TRY(hipEventRecord(w->ev_out, w->s_up));
+    if (cs)
+      HIP_TRY(hipStreamWaitEvent(cs, w->ev_out, 0));
+    else
+      HIP_TRY(hipEventSynchronize(w->ev_out));
+    if (w->strict)
+      if (int e = drain(w)) return e;
+    return 0;
+  };
+  if (int e = go()) return call.done(w->sticky = e);
+  return 0;
+}
+
+int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
+                             uint64_t block_size, const uint8_t *refs) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (total == 0) return 0;
+  if (!ctext || !refs) return call.done(fail(GLFSX_E_ARG, "null argument"));
+  if (block_size == 0 || block_size % 64)
+    return call.done(fail(GLFSX_E_UNSUPPORTED, "decrypt needs block_size %% 64 == 0"));
+  auto go = [&]() -> int {
+    if (!w->ev_in) {
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
+    }
+    const uint64_t nb = (total + block_size - 1) / block_size;
+    const uint64_t slab = std::max<uint64_t>(1, (64ull << 20) / block_size);
+    if (int e = w->h_ctx.ensure(slab * block_size + 64 * slab)) return e;
+    if (int e = w->d_ctx.ensure(slab * block_size + 64)) return e;
+    if (int e = w->d_ptx.ensure(slab * block_size + 64)) return e;
+    if (int e = w->d_rfx.ensure(64 * slab)) return e;
+    for (uint64_t b0 = 0; b0 < nb; b0 += slab) {
+      const uint64_t k = std::min(slab, nb - b0);
+      const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
+      // the staging and temporaries are reused: the previous slab's
+      // upload, decrypt and copy-out (all on s_up) must be done
+      HIP_TRY(hipStreamSynchronize(w->s_up));
+      par_memcpy(w->h_ctx.u8(), static_cast<const uint8_t *>(ctext) + b0 * block_size, bytes);
+      memcpy(w->h_ctx.u8() + bytes, refs + 64 * b0, 64 * k);
+      HIP_TRY(hipMemcpyAsync(w->d_ctx.p, w->h_ctx.p, bytes, hipMemcpyHostToDevice, w->s_up));
+      HIP_TRY(hipMemcpyAsync(w->d_rfx.p, w->h_ctx.u8() + bytes, 64 * k,
+                             hipMemcpyHostToDevice, w->s_up));
+      HIP_TRY(launch_decrypt(w->d_ctx.u8(), w->d_ptx.u8(), k, block_size,
+                             bytes - (k - 1) * block_size, w->d_rfx.u8(), w->s_up));
+      if (int e = write_dev(w, w->d_ptx.u8(), bytes)) return e;
+    }
+    HIP_TRY(hipStreamSynchronize(w->s_up));
+    if (w->strict)
+      if (int e = drain(w)) return e;
+    return 0;
+  };
+  if (int e = go()) return call.done(w->sticky = e);
+  return 0;
+}
+
 int glfsx_writer_set_strict(glfsx_writer *w, int strict) {
   if (!w) return fail(GLFSX_E_ARG, "null writer");
   w->strict = strict != 0;
@@ -919,7 +1063,9 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   if (int e = drain(w)) return call.done(w->sticky = e);
   if (w->partial) {  // blob.go:136-140: the tail block, never padded
     uint8_t ref[64];
-    if (int e = post_one(w, 0, w->salts.raw, w->slot[w->cur].h_in.u8(), w->partial, ref))
+    const WSlot &sl = w->slot[w->cur];
+    if (int e = post_one(w, 0, w->salts.raw, sl.on_dev ? sl.d_in.u8() : sl.h_in.u8(),
+                         w->partial, ref, sl.on_dev))
       return call.done(w->sticky = e);
     if (int e = add_ref(w, 0, ref)) return call.done(w->sticky = e);
     w->size += w->partial;
@@ -944,6 +1090,7 @@ void glfsx_writer_free(glfsx_writer *w) {
     for (auto &sl : w->slot) {
       sl.busy = false;
       sl.nblk = 0;
+      sl.on_dev = false;
       if (sl.dev >= 0 && g_slot_pool.size() < 16 * kMaxSlots)
         g_slot_pool.push_back(sl);  // buffers are reused by the next writer
       else
@@ -968,6 +1115,11 @@ void glfsx_writer_free(glfsx_writer *w) {
       release_stream_scratch(st);
       (void)hipStreamDestroy(st);
     }
+  for (hipEvent_t ev : {w->ev_in, w->ev_out})
+    if (ev) (void)hipEventDestroy(ev);
+  if (w->h_ctx.p) (void)hipHostFree(w->h_ctx.p);
+  for (void *p : {w->d_ctx.p, w->d_ptx.p, w->d_rfx.p})
+    if (p) (void)hipFree(p);
   delete w;
 }
 

@@ -20,11 +20,13 @@
 // it is absent the hashing modes fail with GLFSX_E_UNSUPPORTED; nothing on
 // the write path depends on it.
 #include <dlfcn.h>
+#include <sys/mman.h>
 
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/glfsx.h"
@@ -71,6 +73,34 @@ struct CidHash {
 
 }  // namespace
 
+// Blob bytes live in large arenas (mmap'd, transparent huge pages where the
+// kernel allows): one 1 MiB allocation plus 256 page faults per Post cost
+// more than the write path's whole host round trip.
+struct Arena {
+  std::vector<std::pair<uint8_t *, size_t>> chunks;
+  uint8_t *cur = nullptr;
+  size_t left = 0;
+  uint8_t *alloc(size_t n) {
+    if (n > left) {
+      const size_t sz = std::max<size_t>(n, size_t(256) << 20);
+      void *p = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (p == MAP_FAILED) return nullptr;
+      (void)madvise(p, sz, MADV_HUGEPAGE);
+      chunks.emplace_back(static_cast<uint8_t *>(p), sz);
+      cur = static_cast<uint8_t *>(p);
+      left = sz;
+    }
+    uint8_t *r = cur;
+    const size_t a = (n + 63) & ~size_t(63);
+    cur += std::min(a, left);
+    left -= std::min(a, left);
+    return r;
+  }
+  ~Arena() {
+    for (auto &c : chunks) munmap(c.first, c.second);
+  }
+};
+
 struct glfsx_store {
   uint64_t max_size = 0;
   int mode = GLFSX_STORE_TRUST;
@@ -79,7 +109,8 @@ struct glfsx_store {
   bool keyed = false;
   uint8_t key[32]{};
   std::mutex mu;
-  std::unordered_map<std::string, std::vector<uint8_t>, CidHash> blobs;
+  std::unordered_map<std::string, std::pair<const uint8_t *, uint64_t>, CidHash> blobs;
+  Arena arena;
   uint64_t posts = 0, bytes = 0, hashed = 0;
   std::string err;
 };
@@ -149,11 +180,16 @@ int glfsx_store_post(void *store, int kind, const uint8_t *ref, const void *ctex
   std::string k(reinterpret_cast<const char *>(ref), 32);
   auto it = s->blobs.find(k);
   if (it == s->blobs.end()) {
-    auto &v = s->blobs[k];
-    if (s->keep_data)
-      v.assign(static_cast<const uint8_t *>(ctext), static_cast<const uint8_t *>(ctext) + len);
-    else
-      v.resize(0);
+    uint8_t *p = nullptr;
+    if (s->keep_data && len) {
+      p = s->arena.alloc(len);
+      if (!p) {
+        s->err = "store out of memory";
+        return GLFSX_E_NOMEM;
+      }
+      memcpy(p, ctext, len);
+    }
+    s->blobs.emplace(std::move(k), std::make_pair(p, s->keep_data ? len : 0));
   }
   return 0;
 }
@@ -170,8 +206,8 @@ int glfsx_store_get(glfsx_store *s, const uint8_t cid[32], const void **data,
   std::lock_guard<std::mutex> lk(s->mu);
   auto it = s->blobs.find(std::string(reinterpret_cast<const char *>(cid), 32));
   if (it == s->blobs.end()) return GLFSX_E_STORE;  // blobcache.ErrNotFound
-  *data = it->second.data();
-  *len = it->second.size();
+  *data = it->second.first;
+  *len = it->second.second;
   return 0;
 }
 

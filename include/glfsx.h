@@ -161,6 +161,21 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
  * delivered, so the error comes from the Write that filled the failing block,
  * exactly as blob.go:120-133 returns it. */
 int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n);
+/* blob.go:120-133 Write of n bytes already in device memory (current
+ * device): a GPU producer feeds the Writer without a host round trip.
+ * Ordered after the work already enqueued on `stream` (NULL: d_data is
+ * ready now and the call returns once it has been consumed); work enqueued
+ * on `stream` after the call may reuse d_data. */
+int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
+                              void *stream);
+/* Write the plaintext of a blob's data blocks given as ciphertext: block j
+ * of ctext (host memory, block_size bytes, the last one short,
+ * block_size % 64 == 0) is decrypted on the GPU with the DEK in bytes
+ * [32,64) of refs[64 j] (ref.go:113-126 getF) and the plaintext goes into
+ * the Writer without leaving the device -- blob.go:333-345 Concat's read
+ * side fused with its Writer. */
+int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
+                             uint64_t block_size, const uint8_t *refs);
 /* Deliver the Posts of every complete block written so far (no reference
  * counterpart: the reference never holds a complete block back). */
 int glfsx_writer_flush(glfsx_writer *w);

@@ -177,3 +177,58 @@ def test_writer_across_threads(gpu, O):
         assert root.ref.marshal_binary() == want_root, i
         assert [r for _, r, _ in st.log] == [r for _, r, _, _ in want_posts], i
     assert N.device_count() > 0
+
+
+def test_write_device_mixed_with_host_writes(gpu, O):
+    """glfsx_writer_write_device: bytes from HBM in random pieces, mixed
+    with host writes (the staging moves between host and device), across
+    batch boundaries and index posts; root and Post log == the reference
+    writer's.  The producer stream reuses its buffer right after each call:
+    the writer must have consumed the bytes by then (stream ordering)."""
+    import torch
+    from glfs_amd import _native as N, bigblob
+    bs = 64 << 10
+    size = 1100 * bs + 12345           # > one 64 MiB batch, 1 index node + tail
+    data = O.fill_splitmix(size, 31)
+    want_root, _, _, want_posts = O.create(data, bs)
+    st = bigblob.MemStore(bs)
+    w = bigblob.Machine(bs).new_writer(st, None)
+    s = torch.cuda.Stream()
+    buf = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    rng = random.Random(5)
+    off = 0
+    while off < size:
+        p = min(rng.randrange(1, 6 << 20), size - off)
+        piece = data[off:off + p]
+        if rng.random() < 0.3:
+            w.write(piece)
+        else:
+            with torch.cuda.stream(s):
+                buf[:p].copy_(torch.frombuffer(bytearray(piece), dtype=torch.uint8),
+                              non_blocking=False)
+                w.write_device(buf.data_ptr(), p, ctypes.c_void_p(s.cuda_stream))
+                buf.fill_(0xEE)            # reuse at once, ordered after the write
+        off += p
+    root = w.finish()
+    w.close()
+    assert root.ref.marshal_binary() == want_root
+    assert [(k, r) for k, r, _ in st.log] == [(k, r) for k, r, _, _ in want_posts]
+
+
+def test_concat_write_ctext_vs_oracle(gpu, O):
+    """blob.go:333-345 Concat at 1 MiB blocks over roots of ragged sizes
+    (single-block, multi-block with an index node, empty): the data blocks
+    go to the new Writer as ciphertext and are decrypted on the GPU into its
+    staging; root == the oracle's Create of the joined bytes."""
+    from glfs_amd import bigblob
+    bs = 1 << 20
+    m = bigblob.Machine(bs)
+    st = bigblob.NativeStore(bs, "trust")
+    parts = [O.fill_splitmix(n, 70 + i) for i, n in
+             enumerate([3 * bs + 777, 0, 100, bs, 70 * bs + 5])]
+    roots = [m.create(st, None, p) for p in parts]
+    got = m.concat(st, 4096, None, *roots)
+    want = O.create(b"".join(parts), bs)[0]
+    assert got.ref.marshal_binary() == want
+    assert got.size == sum(map(len, parts))
+    assert bigblob.read_all(st, got) == b"".join(parts)
