@@ -1104,14 +1104,19 @@ __device__ __forceinline__ void quad_addrs(uint32_t (&addr)[28], uint32_t slot,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_quad(KArgs a) {
-  __shared__ uint4 slots[256 * 4];      // 64 B message slot per quad
+// QPW quads (chunks) per workgroup: 256 (1024 lanes, 4 waves per SIMD) or
+// 64 (256 lanes, one wave per SIMD: the chain runs at its latency instead
+// of sharing its SIMD with three more waves; a 2 MiB node spreads over 32
+// CUs instead of 8).
+template <int QPW>
+__global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
+  __shared__ uint4 slots[QPW * 4];      // 64 B message slot per quad
   __shared__ uint32_t passbuf[8];       // the odd subtree passing up a level
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint64_t j = blockIdx.x >> a.split_log2;
   const uint32_t sidx = blockIdx.x & ((1u << a.split_log2) - 1u);
   const uint64_t len = (j + 1 == a.n) ? a.last_len : a.msg_len;
-  constexpr uint64_t kSpan = 256ull << 10;
+  constexpr uint64_t kSpan = uint64_t(QPW) << 10;
   const uint64_t c0b = uint64_t(sidx) * kSpan;
   if (sidx != 0 && c0b >= len) return;  // empty sub-range (uniform)
   const bool whole = len <= kSpan;       // the message fits this workgroup
@@ -1129,7 +1134,7 @@ __global__ __launch_bounds__(1024) void k_quad(KArgs a) {
     const uint64_t coff = uint64_t(quad) << 10;
     const uint32_t clen = uint32_t(min<uint64_t>(mylen - coff, 1024));
     const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
-    const uint32_t ctr = sidx * 256u + quad;  // chunk counter (messages < 4 GiB)
+    const uint32_t ctr = sidx * uint32_t(QPW) + quad;  // chunk counter (messages < 4 GiB)
     const uint8_t *cp = msg + coff + 16u * q;
     uint4 blk[16];
 #pragma unroll
@@ -1620,9 +1625,22 @@ bool quad_enabled() {
 }
 
 // BLAKE3-only pass in quad layout (k_quad): latency-bound launches of at
-// most 16384 chunks, messages of at most 64 x 256 KiB.
+// most 16384 chunks, messages of at most 64 x 256 KiB.  Messages of up to
+// 64 x 64 KiB (4 MiB: index nodes at 1-4 MiB blocks) use 64 quads per
+// workgroup, larger ones 256 (the last workgroup merges <= 64 CVs, one per
+// quad of its own).  GLFSX_QPW=256 forces the wide form (A/B).
+int quad_qpw(uint64_t maxlen) {
+  static const int forced = [] {
+    const char *e = getenv("GLFSX_QPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 256) return 256;
+  return maxlen <= (64ull << 16) ? 64 : 256;
+}
+
 hipError_t launch_quad(KArgs a, uint64_t maxlen, hipStream_t s) {
-  constexpr uint64_t kSpan = 256ull << 10;
+  const int qpw = quad_qpw(maxlen);
+  const uint64_t kSpan = uint64_t(qpw) << 10;
   const uint64_t W = maxlen > kSpan ? (maxlen + kSpan - 1) / kSpan : 1;
   uint32_t sl = 0;
   while ((1ull << sl) < W) ++sl;
@@ -1633,7 +1651,10 @@ hipError_t launch_quad(KArgs a, uint64_t maxlen, hipStream_t s) {
     hipError_t e = scratch_get(&a, a.n << sl, a.n, s);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_quad, dim3(uint32_t(a.n << sl)), dim3(1024), 0, s, a);
+  if (qpw == 64)
+    hipLaunchKernelGGL(k_quad<64>, dim3(uint32_t(a.n << sl)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_quad<256>, dim3(uint32_t(a.n << sl)), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 
