@@ -614,9 +614,10 @@ def concat_leg(N, bs=MIB, size=GIB):
         best = dt if best is None else min(best, dt)
     assert r2.ref == root.ref and r2.size == size
     return {"value": round(size / GIB / best, 2), "unit": "GiB/s", "ms": round(best * 1e3, 1),
-            "what": "bigblob Concat of a 1 GiB blob (1 MiB blocks) in a native store: "
-                    "batched GPU decrypt per tree level from host memory, then the Writer "
-                    "(Python API, bytes through host memory both ways)"}
+            "what": "bigblob Concat of a 1 GiB blob (1 MiB blocks) in a native store: index "
+                    "level decrypted in one batch, data blocks handed to the new Writer as "
+                    "ciphertext and decrypted on the GPU into its staging "
+                    "(glfsx_writer_write_ctext); Python API"}
 
 
 if __name__ == "__main__":
