@@ -65,18 +65,21 @@ struct DevBuf {
 };
 struct PinBuf {
   void *p = nullptr;
+  void *dp = nullptr;  // the same memory as the kernels address it
   size_t cap = 0;
   int ensure(size_t n) {
     if (n <= cap) return 0;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dp = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 4096);
     HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
     cap = want;
+    HIP_TRY(hipHostGetDevicePointer(&dp, p, 0));
     return 0;
   }
   uint8_t *u8() const { return static_cast<uint8_t *>(p); }
+  uint8_t *dptr() const { return static_cast<uint8_t *>(dp); }
 };
 
 // Per-thread device context: the library is reentrant because every host
@@ -87,6 +90,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   DevBuf d_in, d_ct, d_refs, d_lvl_a, d_lvl_b, d_small, d_tree;
   PinBuf h_small;
+  PinBuf h_oin, h_oct, h_oref;  // glfsx_post's one-shot staging
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
@@ -126,7 +130,7 @@ int ctx_get(Ctx **out) {
 // concurrently; N pollers would pin N host cores); the rest block at once,
 // and a poller yields its core between queries.
 constexpr int64_t kSpinNs = 2000000;
-constexpr int kMaxSpinners = 2;
+constexpr int kMaxSpinners = 4;
 std::atomic<int> g_spinners{0};
 hipError_t stream_wait(hipStream_t s) {
   if (g_spinners.fetch_add(1, std::memory_order_relaxed) >= kMaxSpinners) {
@@ -151,6 +155,164 @@ hipError_t stream_wait(hipStream_t s) {
 
 hipStream_t pick_stream(Ctx *c, void *stream) {
   return stream ? static_cast<hipStream_t>(stream) : c->stream;
+}
+
+// ---- One-shot posts (launch_one) ----
+// A post of one message of at most kMaxOneLen bytes from host memory: the
+// bytes sit in pinned staging, the kernel reads them there and writes ctext
+// and ref straight back into pinned staging, so a post is one launch and one
+// wait instead of copy, DEK pass, keystream, CID pass and two copies.
+// Concurrent callers (glfs.Machine is used from many goroutines) are
+// coalesced, group-commit style: a caller that finds a free launch lane
+// becomes the leader, takes every pending request (one workgroup each) into
+// one launch on that lane, hands the leadership on and waits for its launch;
+// the others wait for their request to be marked done or for the
+// leadership.  Up to kOneLanes launches are in flight, each carrying
+// whatever queued while the earlier ones ran.  Per-caller launches would cap
+// the process at GPU_MAX_HW_QUEUES (4) posts in flight.
+// GLFSX_ONE=0 routes one-shot posts through the general passes (A/B runs).
+bool one_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GLFSX_ONE");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+constexpr uint32_t kOneBatch = 1024;
+constexpr int kOneLanes = 4;
+struct OneReq {
+  OneDesc d{};
+  std::atomic<int> done{0};
+  int rc = 0;
+  std::string err;
+};
+struct OneLane {
+  std::atomic<bool> busy{false};
+  hipStream_t s = nullptr;
+  OneDesc *h_desc = nullptr;  // pinned, kOneBatch descriptors
+  OneDesc *d_desc = nullptr;  // the kernel's view of h_desc
+};
+struct OnePoster {
+  int dev = -1;
+  std::mutex mu;
+  std::vector<OneReq *> pending;
+  std::atomic<bool> leader{false};
+  OneLane lane[kOneLanes];
+};
+std::mutex g_posters_mu;
+std::vector<OnePoster *> g_posters;  // one per device, process lifetime
+
+int poster_get(int dev, OnePoster **out) {
+  std::lock_guard<std::mutex> lk(g_posters_mu);
+  for (OnePoster *p : g_posters)
+    if (p->dev == dev) {
+      *out = p;
+      return 0;
+    }
+  auto *p = new OnePoster();
+  p->dev = dev;
+  for (OneLane &l : p->lane) {
+    void *h = nullptr, *d = nullptr;
+    if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(&h, sizeof(OneDesc) * kOneBatch, hipHostMallocDefault) != hipSuccess ||
+        hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      for (OneLane &x : p->lane) {
+        if (x.h_desc) (void)hipHostFree(x.h_desc);
+        if (x.s) (void)hipStreamDestroy(x.s);
+      }
+      if (h) (void)hipHostFree(h);
+      delete p;
+      return fail(GLFSX_E_DEVICE, "one-shot post setup failed on device %d", dev);
+    }
+    l.h_desc = static_cast<OneDesc *>(h);
+    l.d_desc = static_cast<OneDesc *>(d);
+  }
+  g_posters.push_back(p);
+  *out = p;
+  return 0;
+}
+
+int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
+  uint64_t max_len = 0;
+  for (size_t i = 0; i < batch.size(); ++i) {
+    L.h_desc[i] = batch[i]->d;
+    max_len = std::max<uint64_t>(max_len, batch[i]->d.len);
+  }
+  HIP_TRY(launch_one(L.d_desc, uint32_t(batch.size()), max_len, L.s));
+  return 0;
+}
+
+// Post r on device dev (the calling thread's current device); returns when
+// r's ctext and ref are in its staging.
+int one_post(int dev, OneReq *r) {
+  if (r->d.len > kMaxOneLen || (reinterpret_cast<uintptr_t>(r->d.src) & 15))
+    return fail(GLFSX_E_ARG, "one-shot post: bad descriptor");
+  OnePoster *P;
+  if (int e = poster_get(dev, &P)) return e;
+  {
+    std::lock_guard<std::mutex> lk(P->mu);
+    P->pending.push_back(r);
+  }
+  for (uint32_t spins = 0;; ++spins) {
+    if (r->done.load(std::memory_order_acquire)) {
+      if (r->rc) return fail(r->rc, "%s", r->err.c_str());
+      return 0;
+    }
+    bool idle = false;
+    if (P->leader.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
+      OneLane *L = nullptr;
+      for (OneLane &l : P->lane) {
+        bool b = false;
+        if (l.busy.compare_exchange_strong(b, true, std::memory_order_acq_rel)) {
+          L = &l;
+          break;
+        }
+      }
+      std::vector<OneReq *> batch;
+      if (L) {
+        std::lock_guard<std::mutex> lk(P->mu);
+        const size_t k = std::min<size_t>(P->pending.size(), kOneBatch);
+        batch.assign(P->pending.begin(), P->pending.begin() + k);
+        P->pending.erase(P->pending.begin(), P->pending.begin() + k);
+      }
+      int rc = 0;
+      if (!batch.empty()) rc = one_launch(*L, batch);
+      // the next batch may launch on another lane while this one runs
+      P->leader.store(false, std::memory_order_release);
+      if (L) {
+        if (!rc && !batch.empty()) {
+          const hipError_t e = stream_wait(L->s);
+          if (e != hipSuccess)
+            rc = fail(GLFSX_E_DEVICE, "one-shot post: %s", hipGetErrorString(e));
+        }
+        L->busy.store(false, std::memory_order_release);
+        const std::string msg = rc ? tls_err : std::string();
+        // a request's owner may return (and free it) once done is set
+        for (OneReq *b : batch) {
+          b->rc = rc;
+          b->err = msg;
+          b->done.store(1, std::memory_order_release);
+        }
+      }
+      continue;
+    }
+    if (spins < 20000)
+      sched_yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+void one_keys(OneDesc &d, const uint8_t salt[32], const uint8_t *cid_key) {
+  words_from_key(d.salt, salt);
+  if (cid_key) {
+    words_from_key(d.cid_key, cid_key);
+    d.cid_keyed = 1;
+  } else {
+    blake3_iv_words(d.cid_key);
+    d.cid_keyed = 0;
+  }
 }
 
 void salt_words(uint32_t w[8], const uint8_t *salt) {
@@ -326,7 +488,7 @@ struct WSlot {
 // Staging of single synchronous posts (index nodes, a writer's tail block).
 struct OneBuf {
   DevBuf d_in, d_ct, d_ref;
-  PinBuf h_ct, h_ref;
+  PinBuf h_in, h_ct, h_ref;  // h_in: one-shot posts of pageable bytes
   int dev = -1;
 };
 std::mutex g_pool_mu;
@@ -404,11 +566,17 @@ int pin_grow(PinBuf &b, size_t need, size_t keep) {
   size_t want = std::max(need, b.cap * 2);
   void *p = nullptr;
   HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+  void *dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    return fail(GLFSX_E_DEVICE, "hipHostGetDevicePointer failed");
+  }
   if (b.p) {
     if (keep) memcpy(p, b.p, keep);
     (void)hipHostFree(b.p);
   }
   b.p = p;
+  b.dp = dp;
   b.cap = want;
   return 0;
 }
@@ -435,11 +603,36 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
 }
 
 // Post one message from host memory (ref.go:98 post + sink), synchronously,
-// on the writer's hash stream with the writer's own staging.
+// with the writer's own staging: messages of at most kMaxOneLen bytes as a
+// one-shot post (data read in place when it lies 16-B aligned in the pinned
+// buffer `pin`), larger ones on the writer's hash stream.
 int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
              const uint8_t *data, uint64_t n, uint8_t ref[64],
-             bool dev_src = false) {
+             bool dev_src = false, const PinBuf *pin = nullptr) {
   OneBuf &o = w->one;
+  if (!dev_src && n <= kMaxOneLen && one_enabled()) {
+    if (int e = o.h_ct.ensure(n + 64)) return e;
+    if (int e = o.h_ref.ensure(64)) return e;
+    OneReq r;
+    if (pin && pin->dp && ((data - pin->u8()) & 15) == 0) {
+      r.d.src = pin->dptr() + (data - pin->u8());
+    } else {
+      if (int e = o.h_in.ensure(n + 64)) return e;
+      if (n) memcpy(o.h_in.p, data, n);
+      r.d.src = o.h_in.dptr();
+    }
+    r.d.ctext = w->post ? o.h_ct.dptr() : nullptr;
+    r.d.ref = o.h_ref.dptr();
+    r.d.len = uint32_t(n);
+    one_keys(r.d, salt, cidk(w));
+    if (int e = one_post(w->dev, &r)) return e;
+    memcpy(ref, o.h_ref.p, 64);
+    if (w->post) {
+      int rc = w->post(w->post_ctx, kind, ref, o.h_ct.p, n);
+      if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+    }
+    return 0;
+  }
   if (int e = o.d_in.ensure(n + 64)) return e;
   if (int e = o.d_ct.ensure(n + 64)) return e;
   if (int e = o.d_ref.ensure(64)) return e;
@@ -475,19 +668,28 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
 }
 
 // blob.go:165-182
+// A level's node holds only its refs (64 B each); it is zero padded to bs
+// bytes when posted (index.go:33-38), so a one-block blob never touches a
+// bs-byte buffer.
+int post_node(glfsx_writer *w, size_t i, uint8_t r[64]) {
+  std::vector<uint8_t> &v = w->indexes[i];
+  v.resize(w->bs, 0);
+  const int e = post_one(w, 1, w->salts.index, v.data(), w->bs, r);
+  v.clear();
+  return e;
+}
+
 int add_ref(glfsx_writer *w, size_t i, const uint8_t ref[64]) {
   if (w->indexes.size() <= i) {
-    w->indexes.emplace_back(w->bs, 0);
+    w->indexes.emplace_back();
     w->counts.push_back(0);
   }
-  memcpy(w->indexes[i].data() + w->counts[i] * 64, ref, 64);
+  w->indexes[i].insert(w->indexes[i].end(), ref, ref + 64);
   w->counts[i]++;
   if (w->counts[i] < w->bf) return 0;
   uint8_t r2[64];
-  if (int e = post_one(w, 1, w->salts.index, w->indexes[i].data(), w->bs, r2))
-    return e;
+  if (int e = post_node(w, i, r2)) return e;
   w->counts[i] = 0;
-  std::fill(w->indexes[i].begin(), w->indexes[i].end(), 0);
   return add_ref(w, i + 1, r2);
 }
 
@@ -632,8 +834,7 @@ int finish_indexes(glfsx_writer *w, uint8_t out[64]) {
     }
     if (w->counts[i] > 0) {
       uint8_t r[64];
-      if (int e = post_one(w, 1, w->salts.index, w->indexes[i].data(), w->bs, r))
-        return e;
+      if (int e = post_node(w, i, r)) return e;
       if (int e = add_ref(w, i + 1, r)) return e;
     }
   }
@@ -756,6 +957,22 @@ int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
                 (unsigned long long)n, (unsigned long long)kMaxMsgLen);
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
+  if (n <= kMaxOneLen && one_enabled()) {
+    if (int e = c->h_oin.ensure(n + 64)) return e;
+    if (int e = c->h_oct.ensure(n + 64)) return e;
+    if (int e = c->h_oref.ensure(64)) return e;
+    if (n) memcpy(c->h_oin.p, ptext, n);
+    OneReq r;
+    r.d.src = c->h_oin.dptr();
+    r.d.ctext = (ctext_out && n) ? c->h_oct.dptr() : nullptr;
+    r.d.ref = c->h_oref.dptr();
+    r.d.len = uint32_t(n);
+    one_keys(r.d, salt, cid_key);
+    if (int e = one_post(c->dev, &r)) return e;
+    memcpy(ref_out, c->h_oref.p, 64);
+    if (ctext_out && n) memcpy(ctext_out, c->h_oct.p, n);
+    return 0;
+  }
   if (int e = c->d_in.ensure(n + 64)) return e;
   if (int e = c->d_ct.ensure(n + 64)) return e;
   if (int e = c->d_refs.ensure(64)) return e;
@@ -860,7 +1077,7 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   }
   w->post = post;
   w->post_ctx = post_ctx;
-  w->indexes.emplace_back(bs, 0);  // blob.go:111
+  w->indexes.emplace_back();  // blob.go:111 (refs only, see post_node)
   w->counts.push_back(0);
   uint64_t batch_mib = 64;
   if (const char *e = getenv("GLFSX_BATCH_MIB")) batch_mib = std::max(1ull, strtoull(e, nullptr, 10));
@@ -1065,7 +1282,7 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
     uint8_t ref[64];
     const WSlot &sl = w->slot[w->cur];
     if (int e = post_one(w, 0, w->salts.raw, sl.on_dev ? sl.d_in.u8() : sl.h_in.u8(),
-                         w->partial, ref, sl.on_dev))
+                         w->partial, ref, sl.on_dev, &sl.h_in))
       return call.done(w->sticky = e);
     if (int e = add_ref(w, 0, ref)) return call.done(w->sticky = e);
     w->size += w->partial;
@@ -1082,8 +1299,11 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
 void glfsx_writer_free(glfsx_writer *w) {
   if (!w) return;
   (void)hipSetDevice(w->dev);
-  for (hipStream_t st : {w->s_up, w->ws, w->s_down})
-    if (st) (void)hipStreamSynchronize(st);
+  // a writer that never submitted a batch nor took device input, and did
+  // not fail, has nothing in flight (its single posts waited for themselves)
+  if (w->seq || w->ev_in || w->sticky)
+    for (hipStream_t st : {w->s_up, w->ws, w->s_down})
+      if (st) (void)hipStreamSynchronize(st);
   std::vector<hipStream_t> drop;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);

@@ -66,6 +66,26 @@ struct SmallJob {
 };
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
 
+// One-shot posts (ref.go:98-161 for one message of at most kMaxOneLen bytes:
+// a glfs.PostBlob of a small blob, a Writer's tail block, an index node of a
+// small-block blob): DEK, ChaCha20 and CID in one launch, one workgroup per
+// descriptor.  src / ctext / ref may be pinned host memory (device pointers
+// of it): the kernel reads the message once and writes ctext and ref
+// straight into the caller's staging, so a post is one launch and a wait.
+constexpr uint64_t kMaxOneLen = 64ull * 1024;
+struct OneDesc {
+  const uint8_t *src;  // 16-B aligned, device-accessible
+  uint8_t *ctext;      // nullable, device-accessible
+  uint8_t *ref;        // 64 B out: CID || DEK, 4-B aligned
+  uint32_t len;        // <= kMaxOneLen
+  uint32_t cid_keyed;
+  uint32_t salt[8];     // DEK key words
+  uint32_t cid_key[8];  // CID key words (IV when unkeyed)
+};
+// descs: n descriptors in device-accessible memory; max_len bounds their len.
+hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
+                      hipStream_t s);
+
 // Read side: decrypt n contiguous blocks (bs % 64 == 0; the last one
 // last_len bytes) with the DEKs in bytes [32,64) of refs[j] (dense).
 hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,

@@ -1260,6 +1260,170 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
   }
 }
 
+// ---- One-shot posts: a whole message of <= kMaxOneLen bytes per workgroup ----
+// The message is staged once into LDS (zero padded to 64 B), then
+//   DEK  : quad i hashes chunk i from the image (k_quad's quad layout, the
+//          16 blocks' LDS addresses are immediates), the quads' CVs merge
+//          pairwise through `tslot` (left-complete tree, ROOT at the top);
+//   ctext: lane t makes keystream block t (+ k * lanes) with the DEK and XORs
+//          it into the image in place (tail bytes masked: the image past len
+//          stays zero, as BLAKE3's last block needs), then stores it out;
+//   CID  : the same quad hash over the image, now ctext.
+// QUADS = 16 (one wave: messages <= 16 KiB) or 64 (four waves).
+template <int QUADS>
+__device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t img,
+                                         uint32_t ts, uint32_t *passbuf,
+                                         uint32_t len, const uint32_t (&key)[8],
+                                         uint32_t base, uint32_t q, uint32_t quad,
+                                         const uint32_t (&rel)[28]) {
+  const uint32_t C = len ? (len + 1023) >> 10 : 1u;
+  const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
+  const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
+  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+  cl = kq_lo;
+  ch = kq_hi;
+  if (quad < C) {
+    const uint32_t clen = min(len - min(len, quad << 10), 1024u);
+    const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
+    uint32_t addr[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) addr[k] = img + (quad << 10) + rel[k];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      if (uint32_t(b) < nb) {
+        const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
+        uint32_t fl = base;
+        if (b == 0) fl |= kChunkStart;
+        if (uint32_t(b) + 1 == nb) {
+          fl |= kChunkEnd;
+          if (C == 1) fl |= kRoot;
+        }
+        const uint32_t dq = qsel(q, quad, 0u, blen, fl);
+        uint32_t ab[28];
+#pragma unroll
+        for (int k = 0; k < 28; ++k) ab[k] = addr[k] + 64u * b;
+        quad_compress(cl, ch, ivq, dq, ab);
+      }
+    }
+  }
+  uint32_t count = C;
+  while (count > 1) {  // uniform
+    const uint32_t half = count >> 1, odd = count & 1u;
+    __syncthreads();  // the previous level's slots have been read
+    if (quad < count) {
+      if (odd && quad == count - 1) {
+        passbuf[q] = cl;
+        passbuf[4 + q] = ch;
+      } else {
+        // left child: words 0-7 of the parent's slot, right child: 8-15
+        const uint32_t sa = ts + ((quad >> 1) << 6) + ((quad & 1u) << 5) + 4u * q;
+        *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(sa) = cl;
+        *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(sa + 16u) = ch;
+      }
+    }
+    __syncthreads();
+    if (quad < half) {
+      const uint32_t fl = base | kParent | (count == 2 ? kRoot : 0u);
+      cl = kq_lo;
+      ch = kq_hi;
+      const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
+      uint32_t addr[28];
+#pragma unroll
+      for (int k = 0; k < 28; ++k) addr[k] = ts + (quad << 6) + rel[k];
+      quad_compress(cl, ch, ivq, dq, addr);
+    } else if (odd && quad == half) {
+      cl = passbuf[q];
+      ch = passbuf[4 + q];
+    }
+    count = half + odd;
+  }
+}
+
+template <int QUADS>
+__global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
+  __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
+  __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
+  __shared__ uint32_t passbuf[8];
+  __shared__ uint32_t s_dek[8];
+  constexpr uint32_t kLanes = QUADS * 4;
+  const OneDesc *dp = descs + blockIdx.x;
+  const uint8_t *src = dp->src;
+  uint8_t *cto = dp->ctext;
+  uint8_t *refo = dp->ref;
+  const uint32_t len = dp->len;
+  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
+  const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
+  // stage the message, zero padded to a whole 64-B block (one block when empty)
+  const uint32_t padded = len ? (len + 63) & ~63u : 64u;
+  for (uint32_t p = tid * 16u; p < padded; p += kLanes * 16u) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (p + 16u <= len) {
+      v = *reinterpret_cast<const uint4 *>(src + p);
+    } else if (p < len) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t i = 0; p + i < len; ++i) w[i >> 2] |= uint32_t(src[p + i]) << (8 * (i & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    img_u4[p >> 4] = v;
+  }
+  uint32_t rel[28];
+  quad_addrs(rel, 0u, q);
+  __syncthreads();
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
+  uint32_t cl, ch;
+  one_hash<QUADS>(cl, ch, img, ts, passbuf, len, key, kKeyed, q, quad, rel);
+  if (quad == 0) {  // lanes 0-3: DEK words q and 4+q
+    s_dek[q] = cl;
+    s_dek[4 + q] = ch;
+  }
+  __syncthreads();
+  uint32_t dek[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dek[i] = s_dek[i];
+  const uint32_t nks = (len + 63) >> 6;
+  for (uint32_t kb = tid; kb < nks; kb += kLanes) {
+    uint32_t x[16];
+    chacha_block<false>(x, dek, kb);
+    const uint32_t avail = min(len - kb * 64u, 64u);
+    if (avail < 64) mask_tail(x, avail);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint4 v = img_u4[kb * 4 + i];
+      v.x ^= x[4 * i];
+      v.y ^= x[4 * i + 1];
+      v.z ^= x[4 * i + 2];
+      v.w ^= x[4 * i + 3];
+      img_u4[kb * 4 + i] = v;
+    }
+  }
+  __syncthreads();
+  if (cto) {  // ctext out (its stores drain while the CID runs)
+    for (uint32_t p = tid * 16u; p < len; p += kLanes * 16u) {
+      const uint4 v = img_u4[p >> 4];
+      if (p + 16u <= len) {
+        *reinterpret_cast<uint4 *>(cto + p) = v;
+      } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t i = 0; p + i < len; ++i) cto[p + i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
+      }
+    }
+  }
+  uint32_t ckey[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ckey[i] = dp->cid_key[i];
+  one_hash<QUADS>(cl, ch, img, ts, passbuf, len, ckey, dp->cid_keyed ? kKeyed : 0u, q,
+                  quad, rel);
+  if (quad == 0) {
+    uint32_t *r = reinterpret_cast<uint32_t *>(refo);
+    r[q] = cl;
+    r[4 + q] = ch;
+    r[8 + q] = dek[q];
+    r[12 + q] = dek[4 + q];
+  }
+}
+
 // Small blobs (glfs.PostBlob of many blobs that each fit one bigblob block,
 // e.g. BASELINE config 4's 1M x 4 KiB): one lane per blob.  A blob of
 // 0 < len <= block_size has root = post(rawSalt, blob) (blob.go:190-193); the
@@ -1867,6 +2031,17 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;
   return launch_small_pass<true>(a, max_len, s);
+}
+
+hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
+                      hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (max_len > kMaxOneLen) return hipErrorInvalidValue;
+  if (max_len <= 16 * 1024)
+    hipLaunchKernelGGL(k_one<16>, dim3(n), dim3(64), 0, s, descs);
+  else
+    hipLaunchKernelGGL(k_one<64>, dim3(n), dim3(256), 0, s, descs);
+  return hipGetLastError();
 }
 
 hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,

@@ -1,0 +1,124 @@
+"""One-shot posts (launch_one / k_one): a message of at most 64 KiB posted in
+one launch straight from pinned staging, and concurrent callers coalesced into
+one launch (glfsx.cpp one_post).  Every ref and ctext == the oracle's
+ref.go:98 post(); Writers whose tail blocks and index nodes take this route
+(block sizes <= 64 KiB) == the oracle Writer (blob.go:85-206), Post order
+included."""
+import ctypes
+import os
+import random
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EDGES = [0, 1, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 2047, 4096, 4097,
+         16383, 16384, 16385, 32768 + 7, 65535, 65536]
+
+
+def _gpu_post(N, salt, data, cid_key=None):
+    ct = ctypes.create_string_buffer(max(len(data), 1))
+    ref = ctypes.create_string_buffer(64)
+    N.check(N.lib.glfsx_post(salt, data, len(data), ct, ref, cid_key))
+    return ref.raw, ct.raw[:len(data)]
+
+
+@pytest.mark.parametrize("keyed", [False, True])
+def test_one_shot_post_edges(gpu, O, keyed):
+    rng = random.Random(11 + keyed)
+    for n in EDGES:
+        salt = rng.randbytes(32)
+        key = rng.randbytes(32) if keyed else None
+        data = rng.randbytes(n)
+        assert _gpu_post(gpu, salt, data, key) == O.post(salt, data, key), n
+
+
+def test_one_shot_post_unaligned_source(gpu, O):
+    """The caller's bytes at odd addresses (copied into aligned staging)."""
+    rng = random.Random(3)
+    buf = rng.randbytes(70000)
+    salt = rng.randbytes(32)
+    for off, n in [(1, 100), (3, 4096), (7, 65536), (13, 0)]:
+        view = (ctypes.c_char * n).from_buffer_copy(buf[off:off + n]) if n else b""
+        data = bytes(view)
+        assert _gpu_post(gpu, salt, data) == O.post(salt, data), (off, n)
+
+
+@pytest.mark.parametrize("bs", [1024, 4096, 65536])
+def test_writer_small_blocks_one_shot(gpu, O, bs):
+    """Tail blocks and every index node (bs <= 64 KiB) go through one-shot
+    posts: roots and the full Post log (kind, ref, ctext) == the oracle."""
+    from glfs_amd import bigblob
+    rng = random.Random(bs)
+    for size in [0, 1, bs - 1, bs, bs + 1, 3 * bs + 5, (bs // 64 + 2) * bs + 17]:
+        data = rng.randbytes(size)
+        salt = rng.randbytes(32)
+        want_root, _, _, want_posts = O.create(data, bs, salt=salt)
+        st = bigblob.MemStore(bs)
+        w = bigblob.Machine(bs).new_writer(st, salt)
+        w.write(data)
+        root = w.finish()
+        w.close()
+        assert root.ref.marshal_binary() == want_root, (bs, size)
+        assert [(k, r, n) for k, r, n in st.log] == \
+               [(k, r, n) for k, r, n, _ in want_posts], (bs, size)
+        for _, r, _, c in want_posts:
+            assert st.blobs[r[:32]] == c, (bs, size)
+
+
+def test_concurrent_one_shot_posts(gpu, O):
+    """16 threads posting ragged small messages at once (coalesced launches
+    of many workgroups): every result == the oracle."""
+    errors = []
+
+    def worker(t):
+        try:
+            from glfs_amd import _native as N
+            N.check(N.lib.glfsx_set_device(0))
+            rng = random.Random(1000 + t)
+            for _ in range(60):
+                n = rng.choice([0, 5, 64, 1000, 4096, 9000, 20000, 65536])
+                salt = rng.randbytes(32)
+                key = rng.randbytes(32) if rng.random() < 0.3 else None
+                data = rng.randbytes(n)
+                got = _gpu_post(N, salt, data, key)
+                if got != O.post(salt, data, key):
+                    errors.append((t, n))
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+
+
+def test_concurrent_small_creates(gpu, O):
+    """glfs.PostBlob-shaped calls (glfsx_create, one Writer per blob) from 12
+    threads, with the blob type salt: roots == the oracle's Create."""
+    from glfs_amd import _native as N, glfs
+    salt = glfs.Machine().make_salt("blob")
+    bs = 2 << 20
+    errors = []
+
+    def worker(t):
+        try:
+            N.check(N.lib.glfsx_set_device(0))
+            rng = random.Random(77 + t)
+            counts, root = (ctypes.c_uint64 * 2)(), N.glfsx_root()
+            sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
+            for _ in range(40):
+                data = rng.randbytes(rng.choice([0, 9, 4096, 70000]))
+                N.check(N.lib.glfsx_create(bs, bs, salt, None, data, len(data), sink,
+                                           ctypes.byref(counts), ctypes.byref(root)))
+                if bytes(root.ref) != O.create(data, bs, salt=salt)[0]:
+                    errors.append((t, len(data)))
+        except Exception as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+    assert os.environ.get("GLFSX_ONE", "1") != "0"
