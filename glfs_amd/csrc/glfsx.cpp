@@ -852,6 +852,15 @@ const char *glfsx_version(void) { return "glfsx 0.1 gfx950"; }
 uint32_t glfsx_set_split_target(uint32_t wgs) { return set_split_target(wgs); }
 uint32_t glfsx_set_latency_wgs(uint32_t wgs) { return set_latency_wgs(wgs); }
 
+#if GLFSX_WGTIME
+// diagnostic builds only (tools/build_variant.sh): the bulk passes' phase
+// timestamps, 8192 x 8 words
+int glfsx_debug_wgtime(uint64_t *out) {
+  HIP_TRY(debug_wgtime(out));
+  return 0;
+}
+#endif
+
 int glfsx_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

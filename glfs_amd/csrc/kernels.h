@@ -130,6 +130,10 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
 hipError_t launch_fill_blobs(uint8_t *dst, uint64_t n, uint64_t len, uint64_t seed0,
                              hipStream_t s);
 
+#if GLFSX_WGTIME
+hipError_t debug_wgtime(uint64_t *out);  // 8192 x 8 words (diagnostic builds)
+#endif
+
 void words_from_key(uint32_t w[8], const uint8_t key[32]);
 void blake3_iv_words(uint32_t w[8]);
 

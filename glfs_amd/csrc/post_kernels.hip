@@ -919,6 +919,27 @@ __device__ __forceinline__ void tree_reduce(uint32_t *lds, uint32_t k,
   }
 }
 
+#if GLFSX_WGTIME
+// Phase timestamps per workgroup of the bulk passes (A/B diagnostics only,
+// tools/build_variant.sh wgtime "-DGLFSX_WGTIME=1"): [start, chunks done,
+// subtree done, end, HW_ID, XCC_ID, 0, 0]; DEK pass at [0, 4096), CID pass
+// at [4096, 8192).  s_memrealtime: 100 MHz.
+__device__ uint64_t g_wgtime[8192][8];
+__device__ __forceinline__ void wgt(bool chacha, int slot) {
+  const uint32_t b = blockIdx.x + (chacha ? 4096u : 0u);
+  if (threadIdx.x == 0 && b < 8192) {
+    g_wgtime[b][slot] = __builtin_amdgcn_s_memrealtime();
+    if (slot == 0) {
+      g_wgtime[b][4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      g_wgtime[b][5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+  }
+}
+#define WGT(slot) wgt(CHACHA, slot)
+#else
+#define WGT(slot) (void)0
+#endif
+
 // A: ARX in the asm form (many waves per SIMD); false: the compiler's form,
 // which issues faster when a launch leaves a SIMD one or two waves
 template <int G, bool CHACHA, bool ALIGNED, bool A = true>
@@ -929,6 +950,7 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
       (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
   __shared__ uint4 lds_u4[512 + kStageU4];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
+  WGT(0);
   // message j, sub-range sidx (split mode) = chunks [sidx*256G, +256G)
   const uint64_t j = blockIdx.x >> a.split_log2;
   const uint32_t sidx = blockIdx.x & ((1u << a.split_log2) - 1u);
@@ -999,7 +1021,9 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
     for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
   }
   __syncthreads();
+  WGT(1);
   tree_reduce(lds, active, t, key, a.base, !split, cv);
+  WGT(2);
   if (!split) {
     if (t == 0) store_digest(ref + a.out_off, cv);
     return;
@@ -1010,8 +1034,20 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   const uint64_t wbase = j << a.split_log2;
   if (t == 0) publish_cv(a.scratch + (wbase + sidx) * 8, cv);
   const uint32_t W = uint32_t((len_full + kSpan - 1) / kSpan);
-  __shared__ uint32_t s_flag;
-  if (!arrive_last(a.cnt + j, W, t, &s_flag)) return;
+  // the arrival flag lives in the (now idle) staging image: one more LDS
+  // word would take the kernel past 40 KiB, i.e. from four workgroups per
+  // CU to three (160 KiB / 40 KiB)
+  uint32_t *flag;
+  if constexpr (kStageU4 != 0) {
+    flag = reinterpret_cast<uint32_t *>(lds_u4 + 512);
+  } else {
+    __shared__ uint32_t s_flag;
+    flag = &s_flag;
+  }
+  if (!arrive_last(a.cnt + j, W, t, flag)) {
+    WGT(3);
+    return;
+  }
   if (t < W) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1025,6 +1061,7 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
     store_digest(ref + a.out_off, cv);
     a.cnt[j] = 0;
   }
+  WGT(3);
 }
 
 // ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
@@ -2032,6 +2069,13 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   a.out_off = 0;
   return launch_small_pass<true>(a, max_len, s);
 }
+
+#if GLFSX_WGTIME
+hipError_t debug_wgtime(uint64_t *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgtime), sizeof(g_wgtime), 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
                       hipStream_t s) {
