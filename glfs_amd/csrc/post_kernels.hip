@@ -154,8 +154,10 @@ __device__ __forceinline__ uint32_t add3_a(uint32_t a, uint32_t b, uint32_t c) {
 // dependent instructions are always at least 3 (7 fused) independent ones
 // apart.  1 = compiler-visible C form (no hazard nops), 2 = the one-asm-
 // statement-per-instruction form (default: measured +2.5% config 2, +1-2%
-// small blobs and read side, headline unchanged; 1 was 5.7% slower).  0 =
-// the plain macros above.
+// small blobs and read side; 1 was 5.7% slower).  0 = the plain macros
+// above.  The kernels take the form as their int template parameter A
+// (0 = compiler-scheduled C, 1 = asm in quarter-round order, 2 = asm step-
+// interleaved); the headline's CID pass runs form 1 (GLFSX_HEAD_CID).
 #ifndef GLFSX_SCHED
 #define GLFSX_SCHED 2
 #endif
@@ -225,11 +227,11 @@ __device__ __forceinline__ void half_il(uint32_t (&v)[16], const uint32_t (&m)[1
 #undef IL_STEP
 }
 
-template <int R, bool A = true>
+template <int R, int A = 2>
 __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
                                          const uint32_t (&m)[16]) {
 #if GLFSX_SCHED
-  if constexpr (A && R > 0) {
+  if constexpr (A == 2 && R > 0) {
     uint32_t x[16];
     half_il<GLFSX_SCHED, false, R, true, false>(v, m, x);
     half_il<GLFSX_SCHED, true, R, true, false>(v, m, x);
@@ -250,7 +252,7 @@ __device__ __forceinline__ void b3_round(uint32_t (&v)[16],
 // cv <- first 8 words of compress(cv, m, counter, block_len, flags): the
 // chaining value, or for a ROOT compression the first 32 output bytes
 // (XOF block 0), which is all the write path ever reads.
-template <bool A = true>
+template <int A = 2>
 __device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
                                             const uint32_t (&m)[16],
                                             uint32_t ctr_lo, uint32_t ctr_hi,
@@ -280,7 +282,7 @@ __device__ __forceinline__ void b3_compress(uint32_t (&cv)[8],
   b = rotr(b ^ c, 25);
 
 // RFC 8439 block function, nonce 0^12 (ref.go:138), 32-bit block counter.
-template <bool A = true>
+template <int A = 2>
 __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
                                              const uint32_t (&k)[8],
                                              uint32_t ctr) {
@@ -308,7 +310,7 @@ __device__ __forceinline__ void chacha_block(uint32_t (&x)[16],
 #pragma unroll
   for (int i = 1; i < 10; ++i) {
 #if GLFSX_SCHED
-   if constexpr (A) {
+   if constexpr (A == 2) {
     uint32_t v[16], m[16];
     half_il<GLFSX_SCHED, false, 0, false, true>(v, m, x);
     half_il<GLFSX_SCHED, true, 0, false, true>(v, m, x);
@@ -463,7 +465,7 @@ __device__ __forceinline__ bool arrive_last(uint32_t *cnt, uint32_t W,
 
 // Merge step after the last block of local chunk jj: pop/parent/push on the
 // lane's CV stack (eager merges = ctz(jj+1); final merges empty the stack).
-template <int D, bool A = true>
+template <int D, int A = 2>
 __device__ __forceinline__ void lane_merge(uint32_t (&cv)[8],
                                            uint32_t (&stk)[D > 0 ? D : 1][8],
                                            uint32_t &depth, uint32_t jj,
@@ -523,7 +525,7 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   return x;
 }
 
-template <bool CHACHA, bool STAGE = false, bool A = true>
+template <bool CHACHA, bool STAGE = false, int A = 2>
 __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
                                            const uint4 &w1, const uint4 &w2,
                                            const uint4 &w3, uint32_t chunk,
@@ -609,6 +611,7 @@ __device__ __forceinline__ void stage_half(uint32_t wa, uint32_t half,
 // Both blocks of a pair in the LDS-staged CID pass (asm ARX form):
 // ChaCha(a); then BLAKE3(a) interleaved round by round with ChaCha(b);
 // then BLAKE3(b).
+template <int A>
 __device__ __forceinline__ void pair_pipelined(
     uint32_t (&cv)[8], const uint4 &a0, const uint4 &a1, const uint4 &a2,
     const uint4 &a3, const uint4 &b0, const uint4 &b1, const uint4 &b2,
@@ -621,7 +624,7 @@ __device__ __forceinline__ void pair_pipelined(
   const uint32_t ctr_a = (chunk << 4) + blk;
   {
     uint32_t x[16];
-    chacha_block<true>(x, dek, ctr_a);
+    chacha_block<A>(x, dek, ctr_a);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] ^= x[i];
   }
@@ -644,26 +647,29 @@ __device__ __forceinline__ void pair_pipelined(
                     kIV[0], kIV[1], kIV[2], kIV[3], chunk, 0u, 64u, fla};
   b3_round<0, true>(v, m);
 #if GLFSX_SCHED
+  if constexpr (A == 2) {
 #define GQ_IL(R)                                           \
   half_il<GLFSX_SCHED, false, R, true, true>(v, m, x);     \
   half_il<GLFSX_SCHED, true, R, true, true>(v, m, x);
-  GQ_IL(1) GQ_IL(2) GQ_IL(3) GQ_IL(4) GQ_IL(5) GQ_IL(6)
+    GQ_IL(1) GQ_IL(2) GQ_IL(3) GQ_IL(4) GQ_IL(5) GQ_IL(6)
 #undef GQ_IL
-  for (int i = 0; i < 3; ++i) {
-    half_il<GLFSX_SCHED, false, 0, false, true>(v, m, x);
-    half_il<GLFSX_SCHED, true, 0, false, true>(v, m, x);
-  }
-#else
-  gq_round<1>(v, m, x);
-  gq_round<2>(v, m, x);
-  gq_round<3>(v, m, x);
-  gq_round<4>(v, m, x);
-  gq_round<5>(v, m, x);
-  gq_round<6>(v, m, x);
-  CDR_A(x);
-  CDR_A(x);
-  CDR_A(x);
+    for (int i = 0; i < 3; ++i) {
+      half_il<GLFSX_SCHED, false, 0, false, true>(v, m, x);
+      half_il<GLFSX_SCHED, true, 0, false, true>(v, m, x);
+    }
+  } else
 #endif
+  {
+    gq_round<1>(v, m, x);
+    gq_round<2>(v, m, x);
+    gq_round<3>(v, m, x);
+    gq_round<4>(v, m, x);
+    gq_round<5>(v, m, x);
+    gq_round<6>(v, m, x);
+    CDR_A(x);
+    CDR_A(x);
+    CDR_A(x);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
   x[0] += c0;
@@ -678,7 +684,7 @@ __device__ __forceinline__ void pair_pipelined(
 #pragma unroll
   for (int i = 0; i < 16; ++i) mb[i] ^= x[i];
   stage_half(wa, 1, mb);
-  b3_compress<true>(cv, mb, chunk, 0u, 64u, flb);
+  b3_compress<A>(cv, mb, chunk, 0u, 64u, flb);
 }
 
 // Fast path: the lane's G chunks are all full (16*G consecutive 64-B blocks,
@@ -687,7 +693,7 @@ __device__ __forceinline__ void pair_pipelined(
 // next even block's before the odd one, so HBM latency is covered and no
 // buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
 // the chaining-value reset are per-chunk (scalar), not per-block selects.
-template <int G, bool CHACHA, bool STAGE = false, bool A = true>
+template <int G, bool CHACHA, bool STAGE = false, int A = 2>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
@@ -779,7 +785,7 @@ __device__ __forceinline__ void lane_subtree_full(
       if constexpr (GLFSX_PIPE && GLFSX_ASM_ARX == 1 && gl && stg && A) {
         uint32_t fb = base;
         if (pp == 7) fb |= kChunkEnd | ((whole && G == 1) ? kRoot : 0u);
-        pair_pipelined(cv, a0, a1, a2, a3, b0, b1, b2, b3, chunk, 2 * pp,
+        pair_pipelined<A>(cv, a0, a1, a2, a3, b0, b1, b2, b3, chunk, 2 * pp,
                        base | (pp == 0 ? kChunkStart : 0u), fb, dek, wst);
       } else {
       full_block<CHACHA, stg, A>(cv, a0, a1, a2, a3, chunk, 2 * pp,
@@ -823,7 +829,7 @@ __device__ __forceinline__ void lane_subtree_full(
 // its chaining value in cv (or the root output when `whole`: this lane holds
 // the entire message).  Eager merges after chunk jj = ctz(jj+1), final merges
 // right to left: the same tree as BLAKE3's incremental hasher.
-template <int G, bool CHACHA, bool ALIGNED, bool A = true>
+template <int G, bool CHACHA, bool ALIGNED, int A = 2>
 __device__ __forceinline__ void lane_subtree(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint64_t len,
     uint32_t first, uint32_t n_my, bool whole, const uint32_t (&key)[8],
@@ -942,7 +948,7 @@ __device__ __forceinline__ void wgt(bool chacha, int slot) {
 
 // A: ARX in the asm form (many waves per SIMD); false: the compiler's form,
 // which issues faster when a launch leaves a SIMD one or two waves
-template <int G, bool CHACHA, bool ALIGNED, bool A = true>
+template <int G, bool CHACHA, bool ALIGNED, int A = 2>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   // one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext
   // in the CHACHA pass, plaintext in the DEK pass): 40 KiB, 4 WGs per CU
@@ -1479,7 +1485,7 @@ struct SArgs {
   uint32_t out_off;
 };
 
-template <int G, bool CHACHA, bool A = true>
+template <int G, bool CHACHA, int A = 2>
 __global__ __launch_bounds__(256) void k_small(SArgs a) {
   // 4 waves x 8 KiB staging image (same layout as k_pass's)
   __shared__ uint4 lds_u4[4 * 512];
@@ -1570,7 +1576,7 @@ __global__ __launch_bounds__(256) void k_decrypt(KArgs a) {
 // and the loader / storer lane l of instruction k touches image byte
 // 1024k + 16l <-> unit byte 1024k + vo(l).  Covers units [0, n_units);
 // k_decrypt does the rest.
-template <bool A>
+template <int A>
 __global__ __launch_bounds__(256) void k_decrypt_lines(KArgs a, uint64_t n_units,
                                                        uint32_t upb_shift,
                                                        uint32_t run_shift) {
@@ -1707,14 +1713,31 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, uint64_t offset,
 std::atomic<uint32_t> g_latency_wgs{512};
 uint32_t latency_wgs() { return g_latency_wgs.load(std::memory_order_relaxed); }
 
+// ARX form of the many-round launches (no split, G >= 4: the headline's
+// passes): 2 = step-interleaved, 1 = quarter-round order (both one asm
+// statement per instruction).  Split / small-G launches always use 2.
+// Measured (scripts/ab_head.sh, one box, 2 interleaved reps): CID form 1
+// headline 992-995 vs 979-983 GiB/s with form 2, config 2 unchanged
+// (855-860); the DEK pass is indifferent.
+#ifndef GLFSX_HEAD_DEK
+#define GLFSX_HEAD_DEK 2
+#endif
+#ifndef GLFSX_HEAD_CID
+#define GLFSX_HEAD_CID 1
+#endif
+
 template <int G, bool CHACHA>
 hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
   const dim3 grid(uint32_t(a.n << a.split_log2)), block(256);
   // <= 2 waves per SIMD (512 workgroups of 4 waves on 1024 SIMDs): the
   // compiler-scheduled ARX issues faster than the asm form (tools/arx.hip)
   const bool lat = grid.x <= latency_wgs();
+  constexpr int kHead = CHACHA ? GLFSX_HEAD_CID : GLFSX_HEAD_DEK;
   if (aligned && lat)
-    hipLaunchKernelGGL((k_pass<G, CHACHA, true, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_pass<G, CHACHA, true, 0>), grid, block, 0, s, a);
+  else if (kHead != 2 && G >= 4 && aligned && a.split_log2 == 0)
+    hipLaunchKernelGGL((k_pass<G, CHACHA, true, (kHead != 2 ? kHead : 2)>), grid, block, 0,
+                       s, a);
   else if (aligned)
     hipLaunchKernelGGL((k_pass<G, CHACHA, true>), grid, block, 0, s, a);
   else
