@@ -2144,10 +2144,10 @@ hipError_t launch_decrypt(const uint8_t *ctext, uint8_t *ptext, uint64_t n,
     uint64_t grid = (runs + 3) / 4;
     if (grid > 16384) grid = 16384;
     if (grid <= latency_wgs())
-      hipLaunchKernelGGL(k_decrypt_lines<false>, dim3(uint32_t(grid)), dim3(256), 0, s,
+      hipLaunchKernelGGL(k_decrypt_lines<0>, dim3(uint32_t(grid)), dim3(256), 0, s,
                          a, units, upb_shift, run_shift);
     else
-      hipLaunchKernelGGL(k_decrypt_lines<true>, dim3(uint32_t(grid)), dim3(256), 0, s,
+      hipLaunchKernelGGL(k_decrypt_lines<2>, dim3(uint32_t(grid)), dim3(256), 0, s,
                          a, units, upb_shift, run_shift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
