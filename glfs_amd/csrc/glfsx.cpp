@@ -192,7 +192,14 @@ struct OneLane {
   hipStream_t s = nullptr;
   OneDesc *h_desc = nullptr;  // pinned, kOneBatch descriptors
   OneDesc *d_desc = nullptr;  // the kernel's view of h_desc
+  // medium posts: device copies of the messages, and per descriptor
+  // kMedAuxWords words of CVs / arrival counter / DEK (zeroed when grown;
+  // the kernels leave every counter at zero)
+  DevBuf med_msg, med_aux;
+  size_t aux_zeroed = 0;
 };
+constexpr uint64_t kMedBatchBytes = 64ull << 20;  // device copies per launch
+constexpr size_t kMedAuxWords = 64 * 8 + 8 + 8;   // cvs, dek, cnt (+ pad)
 struct OnePoster {
   int dev = -1;
   std::mutex mu;
@@ -233,20 +240,54 @@ int poster_get(int dev, OnePoster **out) {
   return 0;
 }
 
+// One launch of k_one over the batch's small messages and one launch_med
+// (two kernels) over its medium ones, on the lane's stream.
 int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
-  uint64_t max_len = 0;
-  for (size_t i = 0; i < batch.size(); ++i) {
-    L.h_desc[i] = batch[i]->d;
-    max_len = std::max<uint64_t>(max_len, batch[i]->d.len);
+  uint64_t max_small = 0, max_med = 0, med_bytes = 0;
+  size_t ns = 0, nm = 0;
+  for (const OneReq *r : batch) {
+    if (r->d.len <= kMaxOneLen) {
+      ++ns;
+      max_small = std::max<uint64_t>(max_small, r->d.len);
+    } else {
+      ++nm;
+      max_med = std::max<uint64_t>(max_med, r->d.len);
+      med_bytes += (r->d.len + 255) & ~uint64_t(255);
+    }
   }
-  HIP_TRY(launch_one(L.d_desc, uint32_t(batch.size()), max_len, L.s));
+  if (nm) {
+    if (int e = L.med_msg.ensure(med_bytes)) return e;
+    if (int e = L.med_aux.ensure(nm * kMedAuxWords * 4)) return e;
+    if (L.med_aux.cap > L.aux_zeroed) {  // new buffer: counters must start at zero
+      HIP_TRY(hipMemsetAsync(L.med_aux.p, 0, L.med_aux.cap, L.s));
+      L.aux_zeroed = L.med_aux.cap;
+    }
+  }
+  size_t is = 0, im = ns;
+  uint64_t mo = 0;
+  for (const OneReq *r : batch) {
+    if (r->d.len <= kMaxOneLen) {
+      L.h_desc[is++] = r->d;
+      continue;
+    }
+    OneDesc d = r->d;
+    uint32_t *aux = reinterpret_cast<uint32_t *>(L.med_aux.p) + (im - ns) * kMedAuxWords;
+    d.dmsg = L.med_msg.u8() + mo;
+    d.cvs = aux;
+    d.dek = aux + 64 * 8;
+    d.cnt = aux + 64 * 8 + 8;
+    mo += (d.len + 255) & ~uint64_t(255);
+    L.h_desc[im++] = d;
+  }
+  if (ns) HIP_TRY(launch_one(L.d_desc, uint32_t(ns), max_small, L.s));
+  if (nm) HIP_TRY(launch_med(L.d_desc + ns, uint32_t(nm), max_med, L.s));
   return 0;
 }
 
 // Post r on device dev (the calling thread's current device); returns when
 // r's ctext and ref are in its staging.
 int one_post(int dev, OneReq *r) {
-  if (r->d.len > kMaxOneLen || (reinterpret_cast<uintptr_t>(r->d.src) & 15))
+  if (r->d.len > kMaxMedLen || (reinterpret_cast<uintptr_t>(r->d.src) & 15))
     return fail(GLFSX_E_ARG, "one-shot post: bad descriptor");
   OnePoster *P;
   if (int e = poster_get(dev, &P)) return e;
@@ -272,7 +313,18 @@ int one_post(int dev, OneReq *r) {
       std::vector<OneReq *> batch;
       if (L) {
         std::lock_guard<std::mutex> lk(P->mu);
-        const size_t k = std::min<size_t>(P->pending.size(), kOneBatch);
+        // up to kOneBatch requests, at most kMedBatchBytes of medium ones
+        // (always at least one request)
+        size_t k = 0;
+        uint64_t mb = 0;
+        while (k < P->pending.size() && k < kOneBatch) {
+          const uint64_t len = P->pending[k]->d.len;
+          if (len > kMaxOneLen) {
+            if (k && mb + len > kMedBatchBytes) break;
+            mb += len;
+          }
+          ++k;
+        }
         batch.assign(P->pending.begin(), P->pending.begin() + k);
         P->pending.erase(P->pending.begin(), P->pending.begin() + k);
       }
@@ -608,22 +660,25 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
 // buffer `pin`), larger ones on the writer's hash stream.
 int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
              const uint8_t *data, uint64_t n, uint8_t ref[64],
-             bool dev_src = false, const PinBuf *pin = nullptr) {
+             bool dev_src = false, const PinBuf *pin = nullptr,
+             uint64_t present = ~0ull) {
   OneBuf &o = w->one;
-  if (!dev_src && n <= kMaxOneLen && one_enabled()) {
+  if (!dev_src && n <= kMaxMedLen && one_enabled()) {
     if (int e = o.h_ct.ensure(n + 64)) return e;
     if (int e = o.h_ref.ensure(64)) return e;
+    const uint64_t have = std::min(n, present);
     OneReq r;
     if (pin && pin->dp && ((data - pin->u8()) & 15) == 0) {
       r.d.src = pin->dptr() + (data - pin->u8());
     } else {
       if (int e = o.h_in.ensure(n + 64)) return e;
-      if (n) memcpy(o.h_in.p, data, n);
+      if (have) par_memcpy(o.h_in.u8(), data, have);
       r.d.src = o.h_in.dptr();
     }
     r.d.ctext = w->post ? o.h_ct.dptr() : nullptr;
     r.d.ref = o.h_ref.dptr();
     r.d.len = uint32_t(n);
+    r.d.present = uint32_t(have);
     one_keys(r.d, salt, cidk(w));
     if (int e = one_post(w->dev, &r)) return e;
     memcpy(ref, o.h_ref.p, 64);
@@ -673,8 +728,13 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
 // bs-byte buffer.
 int post_node(glfsx_writer *w, size_t i, uint8_t r[64]) {
   std::vector<uint8_t> &v = w->indexes[i];
-  v.resize(w->bs, 0);
-  const int e = post_one(w, 1, w->salts.index, v.data(), w->bs, r);
+  int e;
+  if (w->bs <= kMaxMedLen && one_enabled()) {  // the kernel reads the rest as zero
+    e = post_one(w, 1, w->salts.index, v.data(), w->bs, r, false, nullptr, v.size());
+  } else {
+    v.resize(w->bs, 0);
+    e = post_one(w, 1, w->salts.index, v.data(), w->bs, r);
+  }
   v.clear();
   return e;
 }
@@ -966,16 +1026,17 @@ int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
                 (unsigned long long)n, (unsigned long long)kMaxMsgLen);
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
-  if (n <= kMaxOneLen && one_enabled()) {
+  if (n <= kMaxMedLen && one_enabled()) {
     if (int e = c->h_oin.ensure(n + 64)) return e;
     if (int e = c->h_oct.ensure(n + 64)) return e;
     if (int e = c->h_oref.ensure(64)) return e;
-    if (n) memcpy(c->h_oin.p, ptext, n);
+    if (n) par_memcpy(c->h_oin.u8(), static_cast<const uint8_t *>(ptext), n);
     OneReq r;
     r.d.src = c->h_oin.dptr();
     r.d.ctext = (ctext_out && n) ? c->h_oct.dptr() : nullptr;
     r.d.ref = c->h_oref.dptr();
     r.d.len = uint32_t(n);
+    r.d.present = uint32_t(n);
     one_keys(r.d, salt, cid_key);
     if (int e = one_post(c->dev, &r)) return e;
     memcpy(ref_out, c->h_oref.p, 64);

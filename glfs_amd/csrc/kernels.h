@@ -72,18 +72,30 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
 // descriptor.  src / ctext / ref may be pinned host memory (device pointers
 // of it): the kernel reads the message once and writes ctext and ref
 // straight into the caller's staging, so a post is one launch and a wait.
+// Messages of kMaxOneLen < len <= kMaxMedLen take two launches (launch_med:
+// one workgroup per 64 KiB span, the last-arriving one merges) and need the
+// device scratch below.
 constexpr uint64_t kMaxOneLen = 64ull * 1024;
+constexpr uint64_t kMaxMedLen = 4ull << 20;
 struct OneDesc {
   const uint8_t *src;  // 16-B aligned, device-accessible
-  uint8_t *ctext;      // nullable, device-accessible
+  uint8_t *ctext;      // nullable, device-accessible, 16-B aligned
   uint8_t *ref;        // 64 B out: CID || DEK, 4-B aligned
-  uint32_t len;        // <= kMaxOneLen
+  uint32_t len;        // <= kMaxMedLen
+  uint32_t present;    // bytes [present, len) of the message are zero (not read)
   uint32_t cid_keyed;
   uint32_t salt[8];     // DEK key words
   uint32_t cid_key[8];  // CID key words (IV when unkeyed)
+  // launch_med only (device memory): the staged message (len rounded up to
+  // 64 B), 8 words per 64 KiB span, an arrival counter (zero before the
+  // launch, left at zero) and the DEK
+  uint8_t *dmsg;
+  uint32_t *cvs, *cnt, *dek;
 };
 // descs: n descriptors in device-accessible memory; max_len bounds their len.
 hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
+                      hipStream_t s);
+hipError_t launch_med(const OneDesc *descs, uint32_t n, uint64_t max_len,
                       hipStream_t s);
 
 // Read side: decrypt n contiguous blocks (bs % 64 == 0; the last one

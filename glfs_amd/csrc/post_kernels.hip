@@ -1313,16 +1313,17 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
 //          stays zero, as BLAKE3's last block needs), then stores it out;
 //   CID  : the same quad hash over the image, now ctext.
 // QUADS = 16 (one wave: messages <= 16 KiB) or 64 (four waves).
-template <int QUADS>
-__device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t img,
-                                         uint32_t ts, uint32_t *passbuf,
-                                         uint32_t len, const uint32_t (&key)[8],
-                                         uint32_t base, uint32_t q, uint32_t quad,
-                                         const uint32_t (&rel)[28]) {
+// Messages of up to kMaxMedLen bytes span several such workgroups (64 KiB
+// each) in two launches, k_med_dek and k_med_cid (below).
+
+// Quad `quad` hashes chunk `quad` of the image (len bytes from the image
+// start; chunk counter ctr0 + quad); root: the image is the whole message.
+__device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t img,
+                                           uint32_t len, uint32_t ctr0, bool root,
+                                           uint32_t kq_lo, uint32_t kq_hi, uint32_t ivq,
+                                           uint32_t base, uint32_t q, uint32_t quad,
+                                           const uint32_t (&rel)[28]) {
   const uint32_t C = len ? (len + 1023) >> 10 : 1u;
-  const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
-  const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
-  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
   cl = kq_lo;
   ch = kq_hi;
   if (quad < C) {
@@ -1339,9 +1340,9 @@ __device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t im
         if (b == 0) fl |= kChunkStart;
         if (uint32_t(b) + 1 == nb) {
           fl |= kChunkEnd;
-          if (C == 1) fl |= kRoot;
+          if (root && C == 1) fl |= kRoot;
         }
-        const uint32_t dq = qsel(q, quad, 0u, blen, fl);
+        const uint32_t dq = qsel(q, ctr0 + quad, 0u, blen, fl);
         uint32_t ab[28];
 #pragma unroll
         for (int k = 0; k < 28; ++k) ab[k] = addr[k] + 64u * b;
@@ -1349,7 +1350,16 @@ __device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t im
       }
     }
   }
-  uint32_t count = C;
+}
+
+// Pairwise merge of the `count` CVs held by quads 0..count-1 (left-complete
+// tree) through the parent slots at ts; ROOT on the top parent if root.
+// Every thread of the workgroup calls it (count is uniform).
+__device__ __forceinline__ void one_tree(uint32_t &cl, uint32_t &ch, uint32_t count,
+                                         bool root, uint32_t ts, uint32_t *passbuf,
+                                         uint32_t kq_lo, uint32_t kq_hi, uint32_t ivq,
+                                         uint32_t base, uint32_t q, uint32_t quad,
+                                         const uint32_t (&rel)[28]) {
   while (count > 1) {  // uniform
     const uint32_t half = count >> 1, odd = count & 1u;
     __syncthreads();  // the previous level's slots have been read
@@ -1366,7 +1376,7 @@ __device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t im
     }
     __syncthreads();
     if (quad < half) {
-      const uint32_t fl = base | kParent | (count == 2 ? kRoot : 0u);
+      const uint32_t fl = base | kParent | ((root && count == 2) ? kRoot : 0u);
       cl = kq_lo;
       ch = kq_hi;
       const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
@@ -1382,53 +1392,56 @@ __device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t im
   }
 }
 
-template <int QUADS>
-__global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
-  __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
-  __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
-  __shared__ uint32_t passbuf[8];
-  __shared__ uint32_t s_dek[8];
-  constexpr uint32_t kLanes = QUADS * 4;
-  const OneDesc *dp = descs + blockIdx.x;
-  const uint8_t *src = dp->src;
-  uint8_t *cto = dp->ctext;
-  uint8_t *refo = dp->ref;
-  const uint32_t len = dp->len;
-  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
-  const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
-  // stage the message, zero padded to a whole 64-B block (one block when empty)
+// BLAKE3 (keyed when base has kKeyed) of the image as a whole message, or as
+// the subtree of chunks [ctr0, ctr0 + chunks) when !root.  Result in quad 0:
+// lane q holds words q (cl) and 4+q (ch).
+__device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t img,
+                                         uint32_t ts, uint32_t *passbuf,
+                                         uint32_t len, const uint32_t (&key)[8],
+                                         uint32_t base, uint32_t q, uint32_t quad,
+                                         const uint32_t (&rel)[28], uint32_t ctr0 = 0,
+                                         bool root = true) {
+  const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
+  const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
+  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+  one_chunks(cl, ch, img, len, ctr0, root, kq_lo, kq_hi, ivq, base, q, quad, rel);
+  const uint32_t C = len ? (len + 1023) >> 10 : 1u;
+  one_tree(cl, ch, C, root, ts, passbuf, kq_lo, kq_hi, ivq, base, q, quad, rel);
+}
+
+// Stage bytes [0, len) of a message into the image, zero padded to a whole
+// 64-B block (one block when empty): bytes at and past `present` read as
+// zero (an index node posted from its refs alone).  dcopy (nullable): the
+// staged image is also stored there (the medium path's device copy).
+template <int LANES>
+__device__ __forceinline__ void one_stage(uint4 *img_u4, const uint8_t *src, uint32_t len,
+                                          uint32_t present, uint8_t *dcopy) {
   const uint32_t padded = len ? (len + 63) & ~63u : 64u;
-  for (uint32_t p = tid * 16u; p < padded; p += kLanes * 16u) {
+  const uint32_t have = min(len, present);
+  for (uint32_t p = threadIdx.x * 16u; p < padded; p += LANES * 16u) {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (p + 16u <= len) {
+    if (p + 16u <= have) {
       v = *reinterpret_cast<const uint4 *>(src + p);
-    } else if (p < len) {
+    } else if (p < have) {
       uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t i = 0; p + i < len; ++i) w[i >> 2] |= uint32_t(src[p + i]) << (8 * (i & 3));
+      for (uint32_t i = 0; p + i < have; ++i) w[i >> 2] |= uint32_t(src[p + i]) << (8 * (i & 3));
       v = make_uint4(w[0], w[1], w[2], w[3]);
     }
     img_u4[p >> 4] = v;
+    if (dcopy) *reinterpret_cast<uint4 *>(dcopy + p) = v;
   }
-  uint32_t rel[28];
-  quad_addrs(rel, 0u, q);
-  __syncthreads();
-  uint32_t key[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
-  uint32_t cl, ch;
-  one_hash<QUADS>(cl, ch, img, ts, passbuf, len, key, kKeyed, q, quad, rel);
-  if (quad == 0) {  // lanes 0-3: DEK words q and 4+q
-    s_dek[q] = cl;
-    s_dek[4 + q] = ch;
-  }
-  __syncthreads();
-  uint32_t dek[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) dek[i] = s_dek[i];
+}
+
+// ChaCha20 (key dek, block counter kb0 + local block) XOR of the image's
+// first len bytes in place; the tail is masked so the image past len stays
+// zero.
+template <int LANES>
+__device__ __forceinline__ void one_xor(uint4 *img_u4, uint32_t len, const uint32_t (&dek)[8],
+                                        uint32_t kb0) {
   const uint32_t nks = (len + 63) >> 6;
-  for (uint32_t kb = tid; kb < nks; kb += kLanes) {
+  for (uint32_t kb = threadIdx.x; kb < nks; kb += LANES) {
     uint32_t x[16];
-    chacha_block<false>(x, dek, kb);
+    chacha_block<0>(x, dek, kb0 + kb);
     const uint32_t avail = min(len - kb * 64u, 64u);
     if (avail < 64) mask_tail(x, avail);
 #pragma unroll
@@ -1441,29 +1454,175 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
       img_u4[kb * 4 + i] = v;
     }
   }
-  __syncthreads();
-  if (cto) {  // ctext out (its stores drain while the CID runs)
-    for (uint32_t p = tid * 16u; p < len; p += kLanes * 16u) {
-      const uint4 v = img_u4[p >> 4];
-      if (p + 16u <= len) {
-        *reinterpret_cast<uint4 *>(cto + p) = v;
-      } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        for (uint32_t i = 0; p + i < len; ++i) cto[p + i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
-      }
+}
+
+// Store the image's first len bytes to dst (16-B aligned).
+template <int LANES>
+__device__ __forceinline__ void one_store(const uint4 *img_u4, uint8_t *dst, uint32_t len) {
+  for (uint32_t p = threadIdx.x * 16u; p < len; p += LANES * 16u) {
+    const uint4 v = img_u4[p >> 4];
+    if (p + 16u <= len) {
+      *reinterpret_cast<uint4 *>(dst + p) = v;
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t i = 0; p + i < len; ++i) dst[p + i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
     }
   }
+}
+
+template <int QUADS>
+__global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
+  __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
+  __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
+  __shared__ uint32_t passbuf[8];
+  __shared__ uint32_t s_dek[8];
+  constexpr int kLanes = QUADS * 4;
+  const OneDesc *dp = descs + blockIdx.x;
+  const uint32_t len = dp->len;
+  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
+  const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
+  one_stage<kLanes>(img_u4, dp->src, len, dp->present, nullptr);
+  uint32_t rel[28];
+  quad_addrs(rel, 0u, q);
+  __syncthreads();
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
+  uint32_t cl, ch;
+  one_hash(cl, ch, img, ts, passbuf, len, key, kKeyed, q, quad, rel);
+  if (quad == 0) {  // lanes 0-3: DEK words q and 4+q
+    s_dek[q] = cl;
+    s_dek[4 + q] = ch;
+  }
+  __syncthreads();
+  uint32_t dek[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dek[i] = s_dek[i];
+  one_xor<kLanes>(img_u4, len, dek, 0u);
+  __syncthreads();
+  if (dp->ctext) one_store<kLanes>(img_u4, dp->ctext, len);  // drains during the CID
   uint32_t ckey[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ckey[i] = dp->cid_key[i];
-  one_hash<QUADS>(cl, ch, img, ts, passbuf, len, ckey, dp->cid_keyed ? kKeyed : 0u, q,
-                  quad, rel);
+  one_hash(cl, ch, img, ts, passbuf, len, ckey, dp->cid_keyed ? kKeyed : 0u, q, quad, rel);
   if (quad == 0) {
-    uint32_t *r = reinterpret_cast<uint32_t *>(refo);
+    uint32_t *r = reinterpret_cast<uint32_t *>(dp->ref);
     r[q] = cl;
     r[4 + q] = ch;
     r[8 + q] = dek[q];
     r[12 + q] = dek[4 + q];
+  }
+}
+
+// ---- Medium one-shot posts (kMaxOneLen < len <= kMaxMedLen) ----
+// Workgroup s of a message owns its 64 KiB span s (64 chunks, one per quad).
+// k_med_dek stages the span from the caller's staging (pinned host memory)
+// into LDS and into the descriptor's device copy, hashes its subtree and
+// publishes the CV; the message's last-arriving workgroup merges the W CVs
+// (ROOT on top) into the DEK.  k_med_cid reads the span back from the device
+// copy, XORs the keystream in, stores the ctext to the caller's staging and
+// hashes the CID the same way.  Same cross-XCD protocol as the split passes
+// (publish_cv / arrive_last / load_cv_word); the counter is left at zero.
+// Grid: n x wmax workgroups; workgroups past a message's span exit at once.
+__device__ __forceinline__ void med_publish_merge(uint32_t &cl, uint32_t &ch, const OneDesc *dp,
+                                                  uint32_t sidx, uint32_t W, uint32_t ts,
+                                                  uint32_t *passbuf, uint32_t *flag,
+                                                  const uint32_t (&key)[8], uint32_t base,
+                                                  uint32_t q, uint32_t quad,
+                                                  const uint32_t (&rel)[28], bool *last) {
+  const uint32_t tid = threadIdx.x;
+  if (quad == 0) {  // lanes 0-3 of wave 0: one store instruction per word pair
+    __hip_atomic_store(dp->cvs + sidx * 8 + q, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dp->cvs + sidx * 8 + 4 + q, ch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  *last = arrive_last(dp->cnt, W, tid, flag);
+  if (!*last) return;
+  const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
+  const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
+  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+  if (quad < W) {
+    cl = load_cv_word(dp->cvs + quad * 8 + q);
+    ch = load_cv_word(dp->cvs + quad * 8 + 4 + q);
+  }
+  one_tree(cl, ch, W, true, ts, passbuf, kq_lo, kq_hi, ivq, base, q, quad, rel);
+  if (tid == 0) *dp->cnt = 0;
+}
+
+__global__ __launch_bounds__(256) void k_med_dek(const OneDesc *descs, uint32_t wmax) {
+  __shared__ uint4 img_u4[64 * 64];
+  __shared__ uint4 ts_u4[32 * 4];
+  __shared__ uint32_t passbuf[8];
+  __shared__ uint32_t s_flag;
+  const OneDesc *dp = descs + blockIdx.x / wmax;
+  const uint32_t sidx = blockIdx.x % wmax;
+  const uint32_t len = dp->len;
+  const uint32_t W = (len + 65535u) >> 16;
+  if (sidx >= W) return;  // uniform: past this message's spans
+  const uint32_t off = sidx << 16, slen = min(len - off, 65536u);
+  const uint32_t present = dp->present > off ? dp->present - off : 0u;
+  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
+  const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
+  one_stage<256>(img_u4, dp->src + off, slen, present, dp->dmsg + off);
+  uint32_t rel[28];
+  quad_addrs(rel, 0u, q);
+  __syncthreads();
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
+  uint32_t cl, ch;
+  one_hash(cl, ch, img, ts, passbuf, slen, key, kKeyed, q, quad, rel, sidx << 6, false);
+  bool last;
+  med_publish_merge(cl, ch, dp, sidx, W, ts, passbuf, &s_flag, key, kKeyed, q, quad, rel,
+                    &last);
+  if (last && quad == 0) {
+    dp->dek[q] = cl;
+    dp->dek[4 + q] = ch;
+    uint32_t *r = reinterpret_cast<uint32_t *>(dp->ref);
+    r[8 + q] = cl;
+    r[12 + q] = ch;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t wmax) {
+  __shared__ uint4 img_u4[64 * 64];
+  __shared__ uint4 ts_u4[32 * 4];
+  __shared__ uint32_t passbuf[8];
+  __shared__ uint32_t s_flag;
+  const OneDesc *dp = descs + blockIdx.x / wmax;
+  const uint32_t sidx = blockIdx.x % wmax;
+  const uint32_t len = dp->len;
+  const uint32_t W = (len + 65535u) >> 16;
+  if (sidx >= W) return;
+  const uint32_t off = sidx << 16, slen = min(len - off, 65536u);
+  const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
+  const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
+  // the device copy holds the span zero padded to 64 B (k_med_dek)
+  const uint32_t padded = (slen + 63) & ~63u;
+  for (uint32_t p = tid * 16u; p < padded; p += 256 * 16u)
+    img_u4[p >> 4] = *reinterpret_cast<const uint4 *>(dp->dmsg + off + p);
+  uint32_t dek[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dek[i] = dp->dek[i];
+  uint32_t rel[28];
+  quad_addrs(rel, 0u, q);
+  __syncthreads();
+  one_xor<256>(img_u4, slen, dek, sidx << 10);
+  __syncthreads();
+  if (dp->ctext) one_store<256>(img_u4, dp->ctext + off, slen);
+  uint32_t ckey[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ckey[i] = dp->cid_key[i];
+  const uint32_t base = dp->cid_keyed ? kKeyed : 0u;
+  uint32_t cl, ch;
+  one_hash(cl, ch, img, ts, passbuf, slen, ckey, base, q, quad, rel, sidx << 6, false);
+  bool last;
+  med_publish_merge(cl, ch, dp, sidx, W, ts, passbuf, &s_flag, ckey, base, q, quad, rel,
+                    &last);
+  if (last && quad == 0) {
+    uint32_t *r = reinterpret_cast<uint32_t *>(dp->ref);
+    r[q] = cl;
+    r[4 + q] = ch;
   }
 }
 
@@ -2099,6 +2258,18 @@ hipError_t debug_wgtime(uint64_t *out) {
                              hipMemcpyDeviceToHost);
 }
 #endif
+
+hipError_t launch_med(const OneDesc *descs, uint32_t n, uint64_t max_len,
+                      hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (max_len > kMaxMedLen || max_len <= kMaxOneLen) return hipErrorInvalidValue;
+  const uint32_t wmax = uint32_t((max_len + 65535) >> 16);
+  hipLaunchKernelGGL(k_med_dek, dim3(n * wmax), dim3(256), 0, s, descs, wmax);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_med_cid, dim3(n * wmax), dim3(256), 0, s, descs, wmax);
+  return hipGetLastError();
+}
 
 hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
                       hipStream_t s) {

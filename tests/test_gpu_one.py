@@ -1,8 +1,10 @@
 """One-shot posts (launch_one / k_one): a message of at most 64 KiB posted in
-one launch straight from pinned staging, and concurrent callers coalesced into
-one launch (glfsx.cpp one_post).  Every ref and ctext == the oracle's
+one launch straight from pinned staging; up to 4 MiB in two launches over
+64 KiB spans (launch_med: k_med_dek / k_med_cid, last-arriving workgroup
+merges); concurrent callers coalesced into shared launches (glfsx.cpp
+one_post).  Every ref and ctext == the oracle's
 ref.go:98 post(); Writers whose tail blocks and index nodes take this route
-(block sizes <= 64 KiB) == the oracle Writer (blob.go:85-206), Post order
+(block sizes <= 4 MiB) == the oracle Writer (blob.go:85-206), Post order
 included."""
 import ctypes
 import os
@@ -15,6 +17,8 @@ pytestmark = pytest.mark.gpu
 
 EDGES = [0, 1, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 2047, 4096, 4097,
          16383, 16384, 16385, 32768 + 7, 65535, 65536]
+MEDIUM = [65537, 65536 + 1024, 131072, 131073, 200000, (1 << 20) - 1, 1 << 20,
+          (2 << 20) + 5, (4 << 20) - 64, 4 << 20]
 
 
 def _gpu_post(N, salt, data, cid_key=None):
@@ -34,6 +38,18 @@ def test_one_shot_post_edges(gpu, O, keyed):
         assert _gpu_post(gpu, salt, data, key) == O.post(salt, data, key), n
 
 
+@pytest.mark.parametrize("keyed", [False, True])
+def test_medium_post_edges(gpu, O, keyed):
+    """64 KiB < n <= 4 MiB: the two-launch route (spans of 64 KiB, the last
+    one partial; chunk counters continue across spans)."""
+    rng = random.Random(21 + keyed)
+    for n in MEDIUM:
+        salt = rng.randbytes(32)
+        key = rng.randbytes(32) if keyed else None
+        data = rng.randbytes(n)
+        assert _gpu_post(gpu, salt, data, key) == O.post(salt, data, key), n
+
+
 def test_one_shot_post_unaligned_source(gpu, O):
     """The caller's bytes at odd addresses (copied into aligned staging)."""
     rng = random.Random(3)
@@ -45,13 +61,17 @@ def test_one_shot_post_unaligned_source(gpu, O):
         assert _gpu_post(gpu, salt, data) == O.post(salt, data), (off, n)
 
 
-@pytest.mark.parametrize("bs", [1024, 4096, 65536])
+@pytest.mark.parametrize("bs", [1024, 4096, 65536, 1 << 20, 4 << 20])
 def test_writer_small_blocks_one_shot(gpu, O, bs):
-    """Tail blocks and every index node (bs <= 64 KiB) go through one-shot
-    posts: roots and the full Post log (kind, ref, ctext) == the oracle."""
+    """Tail blocks and every index node (bs <= 4 MiB) go through one-shot
+    posts (index nodes from their refs alone, the rest read as zero): roots
+    and the full Post log (kind, ref, ctext) == the oracle."""
     from glfs_amd import bigblob
     rng = random.Random(bs)
-    for size in [0, 1, bs - 1, bs, bs + 1, 3 * bs + 5, (bs // 64 + 2) * bs + 17]:
+    sizes = [0, 1, bs - 1, bs, bs + 1, 3 * bs + 5]
+    if bs <= 65536:
+        sizes.append((bs // 64 + 2) * bs + 17)  # a full index node, then a second level
+    for size in sizes:
         data = rng.randbytes(size)
         salt = rng.randbytes(32)
         want_root, _, _, want_posts = O.create(data, bs, salt=salt)
@@ -78,7 +98,8 @@ def test_concurrent_one_shot_posts(gpu, O):
             N.check(N.lib.glfsx_set_device(0))
             rng = random.Random(1000 + t)
             for _ in range(60):
-                n = rng.choice([0, 5, 64, 1000, 4096, 9000, 20000, 65536])
+                n = rng.choice([0, 5, 64, 1000, 4096, 9000, 20000, 65536, 70000,
+                                (1 << 20) + 3])
                 salt = rng.randbytes(32)
                 key = rng.randbytes(32) if rng.random() < 0.3 else None
                 data = rng.randbytes(n)
@@ -109,7 +130,8 @@ def test_concurrent_small_creates(gpu, O):
             counts, root = (ctypes.c_uint64 * 2)(), N.glfsx_root()
             sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
             for _ in range(40):
-                data = rng.randbytes(rng.choice([0, 9, 4096, 70000]))
+                data = rng.randbytes(rng.choice([0, 9, 4096, 70000, (1 << 20) + 1,
+                                                 (2 << 20) + 100]))
                 N.check(N.lib.glfsx_create(bs, bs, salt, None, data, len(data), sink,
                                            ctypes.byref(counts), ctypes.byref(root)))
                 if bytes(root.ref) != O.create(data, bs, salt=salt)[0]:
