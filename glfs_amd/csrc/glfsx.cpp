@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <sched.h>
 #include <string>
@@ -286,18 +287,24 @@ int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
 
 // Post r on device dev (the calling thread's current device); returns when
 // r's ctext and ref are in its staging.
-int one_post(int dev, OneReq *r) {
-  if (r->d.len > kMaxMedLen || (reinterpret_cast<uintptr_t>(r->d.src) & 15))
-    return fail(GLFSX_E_ARG, "one-shot post: bad descriptor");
+// Post rs[0..n) on device dev (the calling thread's current device); returns
+// when every request's ctext and ref are in its staging.
+int one_post_many(int dev, OneReq *const *rs, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (rs[i]->d.len > kMaxMedLen || (reinterpret_cast<uintptr_t>(rs[i]->d.src) & 15))
+      return fail(GLFSX_E_ARG, "one-shot post: bad descriptor");
   OnePoster *P;
   if (int e = poster_get(dev, &P)) return e;
   {
     std::lock_guard<std::mutex> lk(P->mu);
-    P->pending.push_back(r);
+    P->pending.insert(P->pending.end(), rs, rs + n);
   }
+  size_t ndone = 0;  // rs[0..ndone) are done
   for (uint32_t spins = 0;; ++spins) {
-    if (r->done.load(std::memory_order_acquire)) {
-      if (r->rc) return fail(r->rc, "%s", r->err.c_str());
+    while (ndone < n && rs[ndone]->done.load(std::memory_order_acquire)) ++ndone;
+    if (ndone == n) {
+      for (size_t i = 0; i < n; ++i)
+        if (rs[i]->rc) return fail(rs[i]->rc, "%s", rs[i]->err.c_str());
       return 0;
     }
     bool idle = false;
@@ -355,6 +362,8 @@ int one_post(int dev, OneReq *r) {
       std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
+
+int one_post(int dev, OneReq *r) { return one_post_many(dev, &r, 1); }
 
 void one_keys(OneDesc &d, const uint8_t salt[32], const uint8_t *cid_key) {
   words_from_key(d.salt, salt);
@@ -633,25 +642,72 @@ int pin_grow(PinBuf &b, size_t need, size_t keep) {
   return 0;
 }
 
-// Host copy into pinned staging; large copies are split over threads (the
-// Writer's memcpy into w.buf, blob.go:121-126, is its host-side cost).
+// Host copy into pinned staging; large copies are split over a persistent
+// pool of copy threads (the Writer's memcpy into w.buf, blob.go:121-126, is
+// its host-side cost: one core copies ≈25 GB/s, a 1 MiB PostBlob spent ≈40
+// µs here).  Pieces of >= 256 KiB; the caller copies one piece itself and
+// spins until the pool has done the rest.  Workers are started on first use
+// (up to 15: the GPU box's share is 16 cores) and live for the process.
+struct CopyTask {
+  uint8_t *dst;
+  const uint8_t *src;
+  size_t n;
+  std::atomic<int> *left;
+};
+struct CopyPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<CopyTask> q;
+  unsigned workers = 0;
+  void run() {
+    for (;;) {
+      CopyTask t;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !q.empty(); });
+        t = q.back();
+        q.pop_back();
+      }
+      memcpy(t.dst, t.src, t.n);
+      t.left->fetch_sub(1, std::memory_order_release);
+    }
+  }
+};
+CopyPool &copy_pool() {
+  static CopyPool *p = [] {
+    auto *cp = new CopyPool();
+    const unsigned hw = std::thread::hardware_concurrency();
+    cp->workers = std::min(15u, hw > 1 ? hw - 1 : 0u);
+    for (unsigned i = 0; i < cp->workers; ++i) std::thread([cp] { cp->run(); }).detach();
+    return cp;
+  }();
+  return *p;
+}
+
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
-  constexpr size_t kMin = 4u << 20;
-  unsigned hw = std::thread::hardware_concurrency();
-  unsigned t = unsigned(std::min<size_t>(std::min(16u, hw ? hw : 1u), n / kMin));
-  if (t <= 1) {
+  constexpr size_t kPiece = 256u << 10;
+  if (n < 2 * kPiece) {
     memcpy(dst, src, n);
     return;
   }
-  std::vector<std::thread> th;
-  const size_t per = (n / t + 4095) & ~size_t(4095);
-  for (unsigned i = 0; i < t; ++i) {
-    const size_t o = i * per;
-    if (o >= n) break;
-    const size_t k = std::min(per, n - o);
-    th.emplace_back([=] { memcpy(dst + o, src + o, k); });
+  CopyPool &P = copy_pool();
+  const size_t parts = std::min<size_t>(P.workers + 1, n / kPiece);
+  if (parts <= 1) {
+    memcpy(dst, src, n);
+    return;
   }
-  for (auto &x : th) x.join();
+  const size_t per = (n / parts + 4095) & ~size_t(4095);
+  std::atomic<int> left{0};
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (size_t o = per; o < n; o += per) {
+      left.fetch_add(1, std::memory_order_relaxed);
+      P.q.push_back({dst + o, src + o, std::min(per, n - o), &left});
+    }
+  }
+  P.cv.notify_all();
+  memcpy(dst, src, std::min(per, n));
+  while (left.load(std::memory_order_acquire) > 0) sched_yield();
 }
 
 // Post one message from host memory (ref.go:98 post + sink), synchronously,
@@ -1209,8 +1265,7 @@ struct WriterCall {
 
 // Drain: submit the staged complete blocks and deliver the Posts of every
 // batch in flight, oldest first.
-int drain(glfsx_writer *w) {
-  if (int e = submit(w)) return e;
+int complete_all(glfsx_writer *w) {
   for (;;) {
     WSlot *o = nullptr;
     for (auto &sl : w->slot)
@@ -1218,6 +1273,61 @@ int drain(glfsx_writer *w) {
     if (!o) return 0;
     if (int e = complete(w, *o)) return e;
   }
+}
+
+int drain(glfsx_writer *w) {
+  if (int e = submit(w)) return e;
+  return complete_all(w);
+}
+
+// Finish with a few complete blocks (<= kFewBlocks) and the tail staged on
+// the host: they go out as one coalesced one-shot post (a request per block)
+// instead of a batch through the three-stream pipeline, so a PostBlob of a
+// few MiB is one launch pair and one wait.  Posts and addRef replay in block
+// order (blob.go:152-163), after every older batch's.
+constexpr uint64_t kFewBlocks = 8;
+int finish_few(glfsx_writer *w, bool *done) {
+  *done = false;
+  WSlot &sl = w->slot[w->cur];
+  if (!one_enabled() || sl.on_dev || w->full == 0 || w->full > kFewBlocks ||
+      w->bs > kMaxMedLen || (w->bs & 15) || !sl.h_in.dp)
+    return 0;
+  if (int e = complete_all(w)) return e;
+  const uint64_t k = w->full + (w->partial ? 1 : 0);
+  OneBuf &o = w->one;
+  if (w->post)
+    if (int e = o.h_ct.ensure(w->full * w->bs + w->partial + 64)) return e;
+  if (int e = o.h_ref.ensure(64 * k)) return e;
+  std::vector<OneReq> reqs(k);
+  std::vector<OneReq *> rp(k);
+  for (uint64_t b = 0; b < k; ++b) {
+    const uint64_t off = b * w->bs;
+    OneDesc &d = reqs[b].d;
+    d.src = sl.h_in.dptr() + off;
+    d.ctext = w->post ? o.h_ct.dptr() + off : nullptr;
+    d.ref = o.h_ref.dptr() + 64 * b;
+    d.len = uint32_t(b < w->full ? w->bs : w->partial);
+    d.present = d.len;
+    one_keys(d, w->salts.raw, cidk(w));
+    rp[b] = &reqs[b];
+  }
+  if (int e = one_post_many(w->dev, rp.data(), k)) return e;
+  // refs out first: an index node posted by add_ref reuses the single-post
+  // staging (its ctext lands on block 0's, already delivered)
+  std::vector<uint8_t> refs(o.h_ref.u8(), o.h_ref.u8() + 64 * k);
+  for (uint64_t b = 0; b < k; ++b) {
+    const uint64_t len = reqs[b].d.len;
+    if (w->post) {
+      int rc = w->post(w->post_ctx, 0, &refs[64 * b], o.h_ct.u8() + b * w->bs, len);
+      if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+    }
+    if (int e = add_ref(w, 0, &refs[64 * b])) return e;
+    w->size += len;
+  }
+  w->full = 0;
+  w->partial = 0;
+  *done = true;
+  return 0;
 }
 }  // namespace
 
@@ -1347,7 +1457,10 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   if (!w || !out) return fail(GLFSX_E_ARG, "null argument");
   WriterCall call(w);
   if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
-  if (int e = drain(w)) return call.done(w->sticky = e);
+  bool few = false;
+  if (int e = finish_few(w, &few)) return call.done(w->sticky = e);
+  if (!few)
+    if (int e = drain(w)) return call.done(w->sticky = e);
   if (w->partial) {  // blob.go:136-140: the tail block, never padded
     uint8_t ref[64];
     const WSlot &sl = w->slot[w->cur];

@@ -59,7 +59,7 @@ int main(int argc, char **argv) {
   const int tmax = argc > 1 ? atoi(argv[1]) : 16;
   const int calls = argc > 2 ? atoi(argv[2]) : 400;
   for (int i = 0; i < 32; i++) salt[i] = (uint8_t)(3 * i + 1);
-  const uint64_t sizes[] = {0, 9, 4096, 65536, 1u << 20};
+  const uint64_t sizes[] = {0, 9, 4096, 65536, 1u << 20, 2u << 20, 3u << 20};
   printf("{");
   for (size_t s = 0; s < sizeof sizes / sizeof sizes[0]; s++) {
     const uint64_t size = sizes[s];
