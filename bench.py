@@ -262,8 +262,8 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
     ms_step = step_ms if step_ms else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": {"dek": "k_pass<4,false,true,true> (keyed BLAKE3, DEK)",
-                       "cid": "k_pass<4,true,true,true> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
+            "kernel": {"dek": "k_pass<4,false,true,2> (keyed BLAKE3, DEK)",
+                       "cid": "k_pass<4,true,true,1> (ChaCha20 + ctext store + BLAKE3 CID)"}[dom],
             "algorithmic_bytes_per_launch": alg[dom],
             "algorithmic_model": "SURVEY 8(d): 1 B of HBM read per plaintext byte hashed",
             "kernel_traffic_frac": (round(traffic / (avg[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
