@@ -525,6 +525,26 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   return x;
 }
 
+// Staging-image swizzle: row L (one lane's pair of blocks, 128 B) keeps its
+// 16-B piece p in slot p ^ img_swz(L).  The three access patterns must be
+// conflict-free: the lane's own ds_write_b128 (groups of 8 consecutive
+// lanes, 32 banks), its ds_read_b128 of its own row, and the store path's
+// ds_read_b128 of (row 8k + l/8, piece l%8) (groups of 16 lanes, 64 banks;
+// MI355X_MICROARCH.md LDS).  (L >> 1) & 7 (GLFSX_SWZ=0) gives pairs of
+// lanes the same slot in the write groups: a 2-way conflict on every staged
+// store (SQ_LDS_BANK_CONFLICT 8.3 cycles per ds_write_b128).  Both keep
+// img_swz(8k + r) = img_swz(r) ^ ((k & 1) << 2), which the store path uses.
+#ifndef GLFSX_SWZ
+#define GLFSX_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t img_swz(uint32_t L) {
+#if GLFSX_SWZ
+  return ((L >> 1) & 3u) | (((L ^ (L >> 3)) & 1u) << 2);
+#else
+  return (L >> 1) & 7u;
+#endif
+}
+
 template <bool CHACHA, bool STAGE = false, int A = 2>
 __device__ __forceinline__ void full_block(uint32_t (&cv)[8], const uint4 &w0,
                                            const uint4 &w1, const uint4 &w2,
@@ -721,9 +741,9 @@ __device__ __forceinline__ void lane_subtree_full(
     a3 = q[3];
   }
   const uint32_t l = threadIdx.x & 63u, r = l >> 3, pc = l & 7u;
-  const uint32_t wa = STAGE ? sbase + (l << 7) + (((l >> 1) & 7u) << 4) : 0u;
+  const uint32_t wa = STAGE ? sbase + (l << 7) + (img_swz(l) << 4) : 0u;
   const uint32_t wst = CHACHA ? wa : 0u;  // full_block's staging target
-  const uint32_t rb = sbase + (r << 7) + ((pc ^ (r >> 1)) << 4);
+  const uint32_t rb = sbase + (r << 7) + ((pc ^ img_swz(r)) << 4);
   // store voffset of (line r of this wave's 8-line group 0, piece pc); lane
   // l's data starts at chunk `first` of msg and lane 0's at first - l*G
   // (k_pass: first = t*G; k_small: msg = the wave's base, first = l*G)
@@ -735,7 +755,7 @@ __device__ __forceinline__ void lane_subtree_full(
       const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
   const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
   // gl: source of (line 8k+r, image slot pc) = piece pc ^ swizzle(8k+r)
-  const uint32_t lo0 = vo - (pc << 4) + ((pc ^ (r >> 1)) << 4);
+  const uint32_t lo0 = vo - (pc << 4) + ((pc ^ img_swz(r)) << 4);
   auto issue = [&](uint32_t s) {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
