@@ -182,6 +182,7 @@ def main():
         hrt = host_round_trip(N, args, bs, barrier, slowest)
         if rank == 0 and world == 1 and args.host_rt_gib > 0:
             out["concat"] = concat_leg(N)
+            out["postblob_latency"] = postblob_latency(N)
         if hrt is not None and world > 1:
             hrt["value"] = round(world * hrt["value"], 2)
             hrt["bytes"] *= world
@@ -585,6 +586,35 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                                  "upstream BLAKE3 C, AVX-512, 1 core)",
                 "trusting_store_keeping_bytes": "pre-hashed Post into a store that copies "
                                                 "every ctext (MemStore's memory cost)"}}
+
+
+def postblob_latency(N, calls=300):
+    """glfs.PostBlob as the drop-in runs it per blob (machine.go:64: one
+    Writer, glfsx_create with the blob type salt at bs 2 MiB, a counting
+    sink): per-call p50 / p90 from one thread (through ctypes; the C harness
+    scripts/latency.c also measures concurrent callers)."""
+    import numpy as np
+    from glfs_amd import glfs
+    salt = glfs.Machine().make_salt("blob")
+    sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
+    counts, root = (ctypes.c_uint64 * 2)(), N.glfsx_root()
+    res = {}
+    for size in (0, 4096, 65536, MIB, 2 * MIB):
+        data = np.frombuffer(np.random.default_rng(size).bytes(max(size, 1)), dtype=np.uint8)
+        ts = []
+        for i in range(calls + 20):
+            t = time.perf_counter()
+            N.check(N.lib.glfsx_create(2 * MIB, 2 * MIB, salt, None, data.ctypes.data, size,
+                                       sink, ctypes.byref(counts), ctypes.byref(root)))
+            if i >= 20:
+                ts.append(time.perf_counter() - t)
+        ts.sort()
+        res[str(size)] = {"p50_us": round(ts[len(ts) // 2] * 1e6, 1),
+                          "p90_us": round(ts[int(len(ts) * 0.9)] * 1e6, 1)}
+    return {"unit": "us per call", "calls": calls, "by_blob_bytes": res,
+            "what": "one glfs.PostBlob (glfsx_create, bs 2 MiB, blob type salt, counting "
+                    "sink) from one Python thread: staging copy, one-shot GPU post "
+                    "(k_one / k_med_*), wait"}
 
 
 def concat_leg(N, bs=MIB, size=GIB):

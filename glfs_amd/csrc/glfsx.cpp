@@ -92,6 +92,7 @@ struct Ctx {
   DevBuf d_in, d_ct, d_refs, d_lvl_a, d_lvl_b, d_small, d_tree;
   PinBuf h_small;
   PinBuf h_oin, h_oct, h_oref;  // glfsx_post's one-shot staging
+  PinBuf h_bin, h_bct, h_bref;  // glfsx_post_blobs' one-shot staging
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
@@ -1794,9 +1795,12 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
     return fail(GLFSX_E_BLOCKSIZE_GT_MAX, "blockSize %llu > maxSize %llu",
                 (unsigned long long)bs, (unsigned long long)store_max);
   if (int e = check_block_size(bs)) return e;
-  // small blobs go through the device batch; larger ones (any size) are
-  // Created one by one through the Writer, their Posts captured
-  std::vector<uint64_t> soffs(n), slens(n);
+  // small blobs go through the device batch; single-block blobs of up to
+  // kMaxMedLen as one-shot posts, kMedBatchBytes at a time (their root is
+  // the block's ref, blob.go:190-193); larger ones Created one by one
+  // through the Writer.  The Posts of the latter two are captured and
+  // delivered in call order below.
+  std::vector<uint64_t> soffs(n), slens(n), med;
   std::vector<std::vector<CapturedPost>> big(n);
   uint64_t span = 0, max_len = 0, n_small = 0;
   for (uint64_t i = 0; i < n; ++i) {
@@ -1807,6 +1811,8 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
       ++n_small;
       span = std::max(span, offsets[i] + lengths[i]);
       max_len = std::max(max_len, lengths[i]);
+    } else if (lengths[i] <= bs && lengths[i] <= kMaxMedLen && one_enabled()) {
+      med.push_back(i);
     } else {
       glfsx_root r;
       if (int e = glfsx_create(bs, store_max, salt, cid_key,
@@ -1818,6 +1824,48 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
   }
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
+  if (!med.empty()) {
+    Salts salts;
+    if (int e = derive_salts(c, salt, &salts)) return e;
+    for (size_t g0 = 0; g0 < med.size();) {
+      size_t g1 = g0;
+      uint64_t bytes = 0;
+      while (g1 < med.size() && (g1 == g0 || bytes + lengths[med[g1]] <= kMedBatchBytes)) {
+        bytes += (lengths[med[g1]] + 63) & ~uint64_t(63);
+        ++g1;
+      }
+      const size_t k = g1 - g0;
+      if (int e = c->h_bin.ensure(bytes)) return e;
+      if (post)
+        if (int e = c->h_bct.ensure(bytes)) return e;
+      if (int e = c->h_bref.ensure(64 * k)) return e;
+      std::vector<OneReq> reqs(k);
+      std::vector<OneReq *> rp(k);
+      uint64_t o = 0;
+      for (size_t j = 0; j < k; ++j) {
+        const uint64_t i = med[g0 + j], len = lengths[i];
+        par_memcpy(c->h_bin.u8() + o, static_cast<const uint8_t *>(data) + offsets[i], len);
+        OneDesc &d = reqs[j].d;
+        d.src = c->h_bin.dptr() + o;
+        d.ctext = post ? c->h_bct.dptr() + o : nullptr;
+        d.ref = c->h_bref.dptr() + 64 * j;
+        d.len = d.present = uint32_t(len);
+        one_keys(d, salts.raw, cid_key);
+        rp[j] = &reqs[j];
+        o += (len + 63) & ~uint64_t(63);
+      }
+      if (int e = one_post_many(c->dev, rp.data(), k)) return e;
+      for (size_t j = 0; j < k; ++j) {
+        const uint64_t i = med[g0 + j];
+        memcpy(roots_out + 64 * i, c->h_bref.u8() + 64 * j, 64);
+        if (post) {
+          const uint64_t off = reqs[j].d.ctext - c->h_bct.dptr();
+          capture_post(&big[i], 0, roots_out + 64 * i, c->h_bct.u8() + off, lengths[i]);
+        }
+      }
+      g0 = g1;
+    }
+  }
   std::vector<uint8_t> h_ct(post ? span + 1 : 0);
   if (n_small) {
     if (int e = c->d_in.ensure(span + 64)) return e;

@@ -734,6 +734,8 @@ def test_post_blobs_mixed_sizes(gpu, O):
         assert refs[i].root.ref.marshal_binary() == want, (i, len(b))
         assert refs[i].root.size == len(b)
         want_log += [(k, r) for k, r, _, _ in posts]
+        for _, r, _, c in posts:             # every ctext the store got
+            assert store.blobs[r[:32]] == c, (i, len(b))
     assert [(k, r) for k, r, _ in store.log] == want_log
     # device-resident: the same roots, ctext of every blob in place
     offs, pos = [], 0
