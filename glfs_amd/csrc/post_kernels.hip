@@ -2099,6 +2099,12 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
   return e;
 }
 
+#ifndef GLFSX_SMALL_DEK
+#define GLFSX_SMALL_DEK 2
+#endif
+#ifndef GLFSX_SMALL_CID
+#define GLFSX_SMALL_CID 2
+#endif
 template <bool CHACHA>
 hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
@@ -2115,12 +2121,14 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
     }
     return hipGetLastError();
   }
+  // ARX form of the many-wave small-blob kernels (GLFSX_SMALL_DEK / _CID)
+  constexpr int F = CHACHA ? GLFSX_SMALL_CID : GLFSX_SMALL_DEK;
   switch (gsel) {
-    case 1: hipLaunchKernelGGL((k_small<1, CHACHA>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_small<2, CHACHA>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_small<4, CHACHA>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_small<8, CHACHA>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_small<16, CHACHA>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_small<1, CHACHA, F>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_small<2, CHACHA, F>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_small<4, CHACHA, F>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_small<8, CHACHA, F>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_small<16, CHACHA, F>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
