@@ -144,3 +144,33 @@ def test_concurrent_small_creates(gpu, O):
     [t.join() for t in th]
     assert not errors, errors[:5]
     assert os.environ.get("GLFSX_ONE", "1") != "0"
+
+
+@pytest.mark.parametrize("fail_at", [1, 2, 3, 4, 5])
+def test_finish_batch_store_error(gpu, O, fail_at):
+    """A Writer finishing with a few staged blocks (one coalesced one-shot
+    batch: 3 blocks + tail, then the index node) and a store whose
+    fail_at-th Post fails: Finish returns the store error after exactly the
+    reference's Posts up to the failing one, in order."""
+    from glfs_amd import bigblob
+    bs = 1 << 20
+    data = O.fill_splitmix(3 * bs + 777, 41)
+    _, _, _, want = O.create(data, bs)
+    assert len(want) == 5
+    log = []
+
+    class Failing:
+        def max_size(self):
+            return bs
+
+        def post(self, ct, ref, kind=0):
+            log.append((kind, ref, bytes(ct)))
+            if len(log) == fail_at:
+                raise IOError("refused")
+
+    w = bigblob.Machine(bs).new_writer(Failing(), None)
+    w.write(data)
+    with pytest.raises(bigblob.StoreError):
+        w.finish()
+    w.close()
+    assert [(k, r, c) for k, r, c in log] == [(k, r, c) for k, r, _, c in want[:fail_at]]
