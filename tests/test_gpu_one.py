@@ -61,8 +61,9 @@ def test_one_shot_post_unaligned_source(gpu, O):
         assert _gpu_post(gpu, salt, data) == O.post(salt, data), (off, n)
 
 
+@pytest.mark.parametrize("keyed", [False, True])
 @pytest.mark.parametrize("bs", [1024, 4096, 65536, 1 << 20, 4 << 20])
-def test_writer_small_blocks_one_shot(gpu, O, bs):
+def test_writer_small_blocks_one_shot(gpu, O, bs, keyed):
     """Tail blocks and every index node (bs <= 4 MiB) go through one-shot
     posts (index nodes from their refs alone, the rest read as zero): roots
     and the full Post log (kind, ref, ctext) == the oracle."""
@@ -74,9 +75,10 @@ def test_writer_small_blocks_one_shot(gpu, O, bs):
     for size in sizes:
         data = rng.randbytes(size)
         salt = rng.randbytes(32)
-        want_root, _, _, want_posts = O.create(data, bs, salt=salt)
+        key = rng.randbytes(32) if keyed else None     # keyed store CID
+        want_root, _, _, want_posts = O.create(data, bs, salt=salt, cid_key=key)
         st = bigblob.MemStore(bs)
-        w = bigblob.Machine(bs).new_writer(st, salt)
+        w = bigblob.Machine(bs).new_writer(st, salt, key)
         w.write(data)
         root = w.finish()
         w.close()
