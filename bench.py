@@ -186,6 +186,8 @@ def main():
         if hrt is not None and world > 1:
             hrt["value"] = round(world * hrt["value"], 2)
             hrt["bytes"] *= world
+            if "sinks" in hrt:   # aggregates too, like value
+                hrt["sinks"] = {k: round(world * v, 2) for k, v in hrt["sinks"].items()}
             hrt["what"] += f"; {world} ranks at once, aggregate over the slowest rank"
         if rank == 0:
             out["host_round_trip"] = hrt

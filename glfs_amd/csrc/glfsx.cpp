@@ -341,9 +341,12 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
       // the next batch may launch on another lane while this one runs
       P->leader.store(false, std::memory_order_release);
       if (L) {
-        if (!rc && !batch.empty()) {
+        // wait even after a failed launch: an earlier kernel of the batch may
+        // still be writing the requests' staging, which their owners reuse
+        // as soon as done is set
+        if (!batch.empty()) {
           const hipError_t e = stream_wait(L->s);
-          if (e != hipSuccess)
+          if (e != hipSuccess && !rc)
             rc = fail(GLFSX_E_DEVICE, "one-shot post: %s", hipGetErrorString(e));
         }
         L->busy.store(false, std::memory_order_release);
