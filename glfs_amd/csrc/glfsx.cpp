@@ -1958,7 +1958,7 @@ int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
   hipStream_t s = pick_stream(c, stream);
-  const uint64_t words = n + (n + 255) / 256 + 1;
+  const uint64_t words = n + (n + kTreeWG - 1) / kTreeWG + 1;
   if (int e = c->d_tree.ensure(8 * words)) return e;
   if (int e = c->h_small.ensure(64)) return e;
   TreeJob j{};

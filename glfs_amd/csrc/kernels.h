@@ -55,6 +55,8 @@ hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
 // (CID || DEK) goes to refs + 64*i (empty blobs use index_salt); longer blobs
 // are skipped (the caller posts them).
 constexpr uint64_t kMaxSmallLen = 16ull * 1024;
+// entries per workgroup of the tree-line kernels (tree_kernels.hip)
+constexpr uint32_t kTreeWG = 256;
 struct SmallJob {
   const uint8_t *src;
   uint8_t *ctext;  // nullable; same offsets as src

@@ -10,11 +10,13 @@
 // numbers, the cid as a hex string (parity unpinned at that one field, see
 // tree.cpp).
 //
-// Layout: one thread per entry.  k_tree_len computes each line's length and
-// a 256-entry workgroup-inclusive scan; k_tree_prefix scans the workgroup
-// totals (one workgroup); k_tree_write builds the workgroup's 256 lines in
-// LDS at the alignment of their destination and stores them with aligned
-// 16-byte stores (bytes at the two partial 16-byte granules of a
+// Layout: one thread per entry, kTreeWG entries per workgroup.  k_tree_len
+// computes each line's length and a workgroup-inclusive scan; k_tree_prefix
+// scans the workgroup totals (one workgroup); k_tree_write builds the
+// workgroup's lines in LDS at the alignment of their destination (the two
+// 64-digit hex fields, 55 % of a config-4 line, as 16-byte words computed
+// four digits per instruction sequence and written with unaligned
+// ds_write_b128) and stores them with aligned 16-byte stores (bytes at the two partial 16-byte granules of a
 // workgroup's span, which it shares with its neighbours, are stored one by
 // one).  A workgroup whose lines do not fit the LDS image stores bytes.
 #include <hip/hip_runtime.h>
@@ -44,8 +46,6 @@ struct TArgs {
 };
 
 constexpr uint32_t kImg = 60 * 1024;  // LDS image per workgroup
-
-__device__ const char kHexD[] = "0123456789abcdef";
 
 // Go's utf8.DecodeRune (see tree.cpp)
 __device__ __forceinline__ void decode_rune(const uint8_t *p, uint64_t n,
@@ -77,51 +77,87 @@ __device__ __forceinline__ void decode_rune(const uint8_t *p, uint64_t n,
   }
 }
 
-// Byte sink: counts, and writes when out != nullptr (LDS or global, through
-// a generic pointer).
-struct Sink {
-  uint8_t *out;
+// Byte sinks.  `line` is instantiated once per sink, so the counting pass
+// touches no output and reads only what lengths depend on, and the LDS
+// writer compiles to ds_write_b8 (no flat stores through a generic pointer).
+struct CountSink {
+  uint32_t o = 0;
+  __device__ __forceinline__ void put(uint8_t) { ++o; }
+  static constexpr bool kWrites = false;
+};
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+struct LdsSink {
+  __attribute__((address_space(3))) uint8_t *p;
   uint32_t o;
-  __device__ __forceinline__ void put(uint8_t c) {
-    if (out) out[o] = c;
-    ++o;
+  __device__ __forceinline__ void put(uint8_t c) { p[o++] = c; }
+  // 16 bytes at any byte offset (LDS accesses may be unaligned on gfx950)
+  __device__ __forceinline__ void put16(u32x4_t v) {
+    typedef __attribute__((address_space(3))) u32x4_t lds_v4
+        __attribute__((aligned(1)));
+    *reinterpret_cast<lds_v4 *>(p + o) = v;
+    o += 16;
   }
-  __device__ __forceinline__ void lit(const char *s) {
-    for (; *s; ++s) put(uint8_t(*s));
-  }
+  static constexpr bool kWrites = true, kWide = true;
+};
+struct GlobalSink {
+  uint8_t *p;
+  uint32_t o;
+  __device__ __forceinline__ void put(uint8_t c) { p[o++] = c; }
+  static constexpr bool kWrites = true, kWide = false;
 };
 
-__device__ void json_string(Sink &k, const uint8_t *s, uint64_t n) {
+template <class S, int N>
+__device__ __forceinline__ void lit(S &k, const char (&s)[N]) {
+  if constexpr (!S::kWrites) {
+    k.o += N - 1;
+  } else {
+#pragma unroll
+    for (int i = 0; i + 1 < N; ++i) k.put(uint8_t(s[i]));
+  }
+}
+
+__device__ __forceinline__ uint8_t hexd(uint32_t v) {
+  return uint8_t(v < 10 ? '0' + v : 'a' - 10 + v);
+}
+
+// One ASCII byte of a JSON string (encoding/json appendString, escapeHTML).
+template <class S>
+__device__ __forceinline__ void put_ascii(S &k, uint32_t b) {
+  if (b >= 0x20 && b != '"' && b != '\\' && b != '<' && b != '>' && b != '&') {
+    k.put(uint8_t(b));
+    return;
+  }
+  k.put('\\');
+  switch (b) {
+    case '"': case '\\': k.put(uint8_t(b)); break;
+    case '\b': k.put('b'); break;
+    case '\f': k.put('f'); break;
+    case '\n': k.put('n'); break;
+    case '\r': k.put('r'); break;
+    case '\t': k.put('t'); break;
+    default:
+      k.put('u'); k.put('0'); k.put('0');
+      k.put(hexd(b >> 4)); k.put(hexd(b & 15));
+  }
+}
+
+template <class S>
+__device__ void json_string(S &k, const uint8_t *s, uint64_t n) {
   k.put('"');
   for (uint64_t i = 0; i < n;) {
     const uint8_t b = s[i];
     if (b < 0x80) {
-      if (b >= 0x20 && b != '"' && b != '\\' && b != '<' && b != '>' && b != '&') {
-        k.put(b);
-      } else {
-        k.put('\\');
-        switch (b) {
-          case '"': case '\\': k.put(b); break;
-          case '\b': k.put('b'); break;
-          case '\f': k.put('f'); break;
-          case '\n': k.put('n'); break;
-          case '\r': k.put('r'); break;
-          case '\t': k.put('t'); break;
-          default:
-            k.put('u'); k.put('0'); k.put('0');
-            k.put(uint8_t(kHexD[b >> 4])); k.put(uint8_t(kHexD[b & 15]));
-        }
-      }
+      put_ascii(k, b);
       ++i;
       continue;
     }
     uint32_t r, sz;
     decode_rune(s + i, n - i, &r, &sz);
     if (r == 0xFFFD && sz == 1) {
-      k.lit("\\ufffd");
+      lit(k, "\\ufffd");
     } else if (r == 0x2028 || r == 0x2029) {
-      k.lit("\\u202");
-      k.put(uint8_t(kHexD[r & 15]));
+      lit(k, "\\u202");
+      k.put(hexd(r & 15));
     } else {
       for (uint32_t q = 0; q < sz; ++q) k.put(s[i + q]);
     }
@@ -130,52 +166,102 @@ __device__ void json_string(Sink &k, const uint8_t *s, uint64_t n) {
   k.put('"');
 }
 
-__device__ void dec(Sink &k, uint64_t v) {
+// decimal digits of v (32-bit arithmetic while it fits)
+template <class S>
+__device__ void dec(S &k, uint64_t v) {
   uint8_t t[20];
   int c = 0;
-  do {
+  while (v >> 32) {
     t[c++] = uint8_t('0' + v % 10);
     v /= 10;
-  } while (v);
-  while (c) k.put(t[--c]);
-}
-
-__device__ void hex32(Sink &k, const uint8_t *x) {
-  k.put('"');
-  for (int i = 0; i < 32; ++i) {
-    k.put(uint8_t(kHexD[x[i] >> 4]));
-    k.put(uint8_t(kHexD[x[i] & 15]));
   }
-  k.put('"');
+  uint32_t w = uint32_t(v);
+  do {
+    t[c++] = uint8_t('0' + w % 10);
+    w /= 10;
+  } while (w);
+  if constexpr (!S::kWrites) {
+    k.o += c;
+  } else {
+    while (c) k.put(t[--c]);
+  }
 }
 
-__device__ uint32_t line(const TArgs &a, uint64_t i, uint8_t *out) {
-  Sink k{out, 0};
-  k.lit("{\"name\":");
+// Lower-case hex digits of bytes b0, b1 (bits 0-15 of x) as four ASCII bytes
+// in output order (hi(b0) lo(b0) hi(b1) lo(b1)), little-endian.
+__device__ __forceinline__ uint32_t hex4(uint32_t x) {
+  const uint32_t n = ((x >> 4) & 0xFu) | ((x & 0xFu) << 8) |
+                     ((x >> 12) & 0xFu) << 16 | ((x >> 8) & 0xFu) << 24;
+  const uint32_t ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;  // nibble >= 10
+  return n + 0x30303030u + ge10 * 39u;  // '0' + n, or 'a' - 10 + n
+}
+
+// "<64 hex digits>" of the 32 bytes at x (one 64-B ref holds two: aligned
+// refs are read as 16-B words)
+template <class S>
+__device__ __forceinline__ void hex32(S &k, const uint8_t *x, bool aligned) {
+  if constexpr (!S::kWrites) {
+    k.o += 66;
+  } else {
+    uint32_t w[8];
+    if (aligned) {
+      const uint4 *q = reinterpret_cast<const uint4 *>(x);
+      const uint4 a = q[0], b = q[1];
+      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+      w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        w[i] = uint32_t(x[4 * i]) | (uint32_t(x[4 * i + 1]) << 8) |
+               (uint32_t(x[4 * i + 2]) << 16) | (uint32_t(x[4 * i + 3]) << 24);
+    }
+    k.put('"');
+    if constexpr (S::kWide) {
+#pragma unroll
+      for (int i = 0; i < 8; i += 2)
+        k.put16(u32x4_t{hex4(w[i]), hex4(w[i] >> 16), hex4(w[i + 1]), hex4(w[i + 1] >> 16)});
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t lo = hex4(w[i]), hi = hex4(w[i] >> 16);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) k.put(uint8_t(lo >> (8 * b)));
+#pragma unroll
+        for (int b = 0; b < 4; ++b) k.put(uint8_t(hi >> (8 * b)));
+      }
+    }
+    k.put('"');
+  }
+}
+
+template <class S>
+__device__ uint32_t line(const TArgs &a, uint64_t i, S k) {
+  lit(k, "{\"name\":");
   json_string(k, a.names + a.name_offs[i], a.name_offs[i + 1] - a.name_offs[i]);
-  k.lit(",\"mode\":");
+  lit(k, ",\"mode\":");
   dec(k, a.modes[i]);
-  k.lit(",\"ref\":{\"type\":");
+  lit(k, ",\"ref\":{\"type\":");
   json_string(k, a.types + a.type_offs[i], a.type_offs[i + 1] - a.type_offs[i]);
-  k.lit(",\"cid\":");
-  hex32(k, a.roots + 64 * i);
-  k.lit(",\"dek\":");
-  hex32(k, a.roots + 64 * i + 32);
-  k.lit(",\"size\":");
+  const bool al = (reinterpret_cast<uintptr_t>(a.roots) & 15) == 0;
+  lit(k, ",\"cid\":");
+  hex32(k, a.roots + 64 * i, al);
+  lit(k, ",\"dek\":");
+  hex32(k, a.roots + 64 * i + 32, al);
+  lit(k, ",\"size\":");
   dec(k, a.sizes[i]);
-  k.lit(",\"blockSize\":");
+  lit(k, ",\"blockSize\":");
   dec(k, a.block_sizes[i]);
-  k.lit("}}\n");
+  lit(k, "}}\n");
   return k.o;
 }
 
-__global__ __launch_bounds__(256) void k_tree_len(TArgs a) {
-  __shared__ uint64_t s[256];
-  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  uint64_t v = i < a.n ? line(a, i, nullptr) : 0;
+__global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
+  __shared__ uint64_t s[kTreeWG];
+  const uint64_t i = uint64_t(blockIdx.x) * kTreeWG + threadIdx.x;
+  uint64_t v = i < a.n ? line(a, i, CountSink{}) : 0;
   s[threadIdx.x] = v;
   __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+  for (uint32_t d = 1; d < kTreeWG; d <<= 1) {  // Hillis-Steele inclusive scan
     const uint64_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
     __syncthreads();
     v += add;
@@ -183,7 +269,7 @@ __global__ __launch_bounds__(256) void k_tree_len(TArgs a) {
     __syncthreads();
   }
   if (i < a.n) a.local_end[i] = v;
-  if (threadIdx.x == 255) a.wg_total[blockIdx.x] = v;
+  if (threadIdx.x == kTreeWG - 1) a.wg_total[blockIdx.x] = v;
 }
 
 // One workgroup: wg_total[0..m) -> exclusive prefix, in chunks of 1024.
@@ -211,11 +297,11 @@ __global__ __launch_bounds__(1024) void k_tree_prefix(uint64_t *t, uint64_t m,
   if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ __launch_bounds__(256) void k_tree_write(TArgs a) {
+__global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a) {
   __shared__ uint4 img4[kImg / 16];
   uint8_t *img = reinterpret_cast<uint8_t *>(img4);
-  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  const uint64_t last = min<uint64_t>(uint64_t(blockIdx.x) * 256 + 255, a.n - 1);
+  const uint64_t i = uint64_t(blockIdx.x) * kTreeWG + threadIdx.x;
+  const uint64_t last = min<uint64_t>(uint64_t(blockIdx.x) * kTreeWG + kTreeWG - 1, a.n - 1);
   const uint64_t base = a.wg_total[blockIdx.x];   // exclusive prefix
   const uint64_t span = a.local_end[last];        // this workgroup's bytes
   const uint32_t sh = uint32_t((reinterpret_cast<uintptr_t>(a.out) + base) & 15);
@@ -224,16 +310,17 @@ __global__ __launch_bounds__(256) void k_tree_write(TArgs a) {
   const uint64_t start = (i < a.n && threadIdx.x) ? a.local_end[i - 1] : 0;
   if (i < a.n && a.line_ends) a.line_ends[i] = base + end;
   if (span + sh > kImg) {  // uniform: lines too long for the image
-    if (i < a.n) line(a, i, a.out + base + start);
+    if (i < a.n) line(a, i, GlobalSink{a.out + base + start, 0});
     return;
   }
-  if (i < a.n) line(a, i, img + sh + start);
+  if (i < a.n)
+    line(a, i, LdsSink{(__attribute__((address_space(3))) uint8_t *)img + sh + start, 0});
   __syncthreads();
   // image byte x <-> out byte base - sh + x; granules [16g, 16g+16)
   uint8_t *dst = a.out + base - sh;
   const uint32_t tot = uint32_t(span) + sh;
   const uint32_t ng = (tot + 15) / 16;
-  for (uint32_t g = threadIdx.x; g < ng; g += 256) {
+  for (uint32_t g = threadIdx.x; g < ng; g += kTreeWG) {
     const uint32_t lo = 16 * g, hi = lo + 16;
     if (lo >= sh && hi <= tot) {
       *reinterpret_cast<uint4 *>(dst + lo) = img4[g];
@@ -278,20 +365,20 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
   a.sizes = j.sizes;
   a.block_sizes = j.block_sizes;
   a.local_end = j.scratch;
-  const uint64_t wgs = (j.n + 255) / 256;
+  const uint64_t wgs = (j.n + kTreeWG - 1) / kTreeWG;
   a.wg_total = j.scratch + j.n;
   a.line_ends = j.line_ends;
   a.out = j.out;
   a.cap = j.cap;
   a.total = j.total;
-  hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
                      j.total);
   e = hipGetLastError();
   if (e != hipSuccess || !j.out) return e;
-  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,7 +1,8 @@
 """Secondary legs alone, for per-kernel profiling (rocprofv3 PMC passes):
 config 4's small-blob kernels (bench.small_blobs) and the read side
-(batched getF decrypt over a --gib GiB blob at 1 MiB blocks).
-usage: python scripts/legs.py [small|read|both] [--gib G]"""
+(batched getF decrypt over a --gib GiB blob at 1 MiB blocks), and config 4
+end to end (bench.config4_end_to_end: blobs, tree lines, tree blob).
+usage: python scripts/legs.py [small|read|both|config4] [--gib G]"""
 import ctypes
 import json
 import os
@@ -35,6 +36,8 @@ def main():
         stream.synchronize()
         roof, _ = bench.roofline(torch, N, data, ct, per, bs, stream, sp)
         out["read_side"] = roof["read_side"]
+    if what == "config4":
+        out["config4_end_to_end"] = bench.config4_end_to_end(torch, N, stream, sp)
     print(json.dumps(out), flush=True)
 
 
