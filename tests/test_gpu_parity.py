@@ -573,14 +573,18 @@ def test_post_blobs_device_config4_sample(gpu, O):
         assert rh[64 * i:64 * i + 64] == want, i
 
 
+@pytest.mark.parametrize("bulk", [False, True])
 @pytest.mark.parametrize("ln", [1024, 2048, 4096, 16384])
-def test_post_blobs_dense_vs_scattered(gpu, O, ln):
+def test_post_blobs_dense_vs_scattered(gpu, O, latency_wgs, ln, bulk):
     """Densely packed equal blobs take the LDS-staged wave path of k_small;
     the same blobs at permuted offsets take the per-lane path.  Every root
     and every ctext byte must agree (and sampled roots with the oracle), with
-    and without ctext, with a partial last wave."""
+    and without ctext, with a partial last wave; latency-mode launches (the
+    compiler's ARX form) and bulk ones (latency threshold 0)."""
     torch = _torch()
     from glfs_amd import _native as N
+    if bulk:
+        latency_wgs(0)
     n = 64 * 5 + 17
     rng = random.Random(ln)
     perm = list(range(n))
@@ -615,6 +619,41 @@ def test_post_blobs_dense_vs_scattered(gpu, O, ln):
         want, _, _, posts = O.create(data[i * ln:(i + 1) * ln], 2 << 20, salt=blob_salt)
         assert ra[64 * i:64 * i + 64] == want, i
         assert ca[i * ln:(i + 1) * ln] == posts[0][3], i
+
+
+def test_post_blobs_bulk_mixed_vs_oracle(gpu, O, latency_wgs):
+    """k_small in a bulk launch (the asm ARX form) over blobs of at most 4 KiB:
+    waves of densely packed 4 KiB blobs (LDS-staged), waves mixing them with
+    ragged, empty and unaligned blobs (per-lane paths), and a partial last
+    wave; every root and ctext byte against the oracle."""
+    torch = _torch()
+    from glfs_amd import _native as N
+    latency_wgs(0)
+    rng = random.Random(23)
+    lens = [4096] * 320 + [0, 1, 63, 64, 1024, 2049, 4095, 4096, 4096, 3000]
+    lens += [rng.choice([4096, rng.randrange(0, 4097)]) for _ in range(300)] + [4096] * 77
+    offs, o = [], 0
+    for i, n in enumerate(lens):
+        if i >= 320 and rng.random() < 0.3:
+            o += rng.randrange(1, 16)          # unaligned / scattered blobs
+        offs.append(o)
+        o += n
+    total = o
+    src = dev_bytes(torch, total + 64, seed=29)
+    ct = zeros(torch, total + 64)
+    roots = zeros(torch, 64 * len(lens))
+    d_offs = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    d_lens = torch.tensor(lens, dtype=torch.int64, device="cuda")
+    blob_salt = O.derive_key(bytes(32), b"blob")
+    N.check(N.lib.glfsx_post_blobs_device(2 << 20, blob_salt, None, src.data_ptr(),
+                                          d_offs.data_ptr(), d_lens.data_ptr(), len(lens),
+                                          max(lens), ct.data_ptr(), roots.data_ptr(), None))
+    torch.cuda.synchronize()
+    data, ch, rh = host(src, total), host(ct, total), host(roots, 64 * len(lens))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        want, _, _, posts = O.create(data[o:o + n], 2 << 20, salt=blob_salt)
+        assert rh[64 * i:64 * i + 64] == want, (i, n)
+        assert ch[o:o + n] == posts[0][3], (i, n)
 
 
 # ---------------------------------------------------------------- read side
