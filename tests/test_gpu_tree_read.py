@@ -227,9 +227,10 @@ def _dev_arr(torch, vals, dtype):
     return torch.tensor(vals, dtype=dtype, device="cuda")
 
 
-def _encode_device(torch, ents, out_shift=0, cap=None, want_ends=True):
-    """glfsx_tree_encode_device over entries copied to HBM; returns (bytes,
-    line_ends) or raises GlfsxError."""
+def _encode_device(torch, ents, out_shift=0, cap=None, want_ends=True, roots_shift=0):
+    """glfsx_tree_encode_device over entries copied to HBM (the roots array
+    roots_shift bytes past a 16-B boundary); returns (bytes, line_ends) or
+    raises GlfsxError."""
     import ctypes
     from glfs_amd import _native as N, tree as T
     n = len(ents)
@@ -247,7 +248,8 @@ def _encode_device(torch, ents, out_shift=0, cap=None, want_ends=True):
     d_names, d_types = u8(b"".join(names)), u8(b"".join(types))
     d_no, d_to = _dev_arr(torch, offs(names), torch.int64), _dev_arr(torch, offs(types), torch.int64)
     d_modes = _dev_arr(torch, [e.file_mode for e in ents], torch.int64).to(torch.int32)
-    d_roots = u8(b"".join(e.ref.root.ref.cid + e.ref.root.ref.dek for e in ents))
+    d_roots = u8(bytes(roots_shift) + b"".join(e.ref.root.ref.cid + e.ref.root.ref.dek
+                                              for e in ents))[roots_shift:]
     d_sizes = _dev_arr(torch, [e.ref.root.size for e in ents], torch.int64)
     d_bss = _dev_arr(torch, [e.ref.root.block_size for e in ents], torch.int64)
     total = ctypes.c_uint64()
@@ -278,7 +280,7 @@ def _encode_device(torch, ents, out_shift=0, cap=None, want_ends=True):
 
 def test_tree_encode_device_vs_host(gpu):
     """k_tree_len/prefix/write == the host encoder == entry_json_line, for
-    every escaping class, several destination alignments, lines too long
+    every escaping class, several destination and roots alignments, lines too long
     for a workgroup's LDS image, and a too-small buffer (an error, nothing
     written)."""
     import torch
@@ -301,6 +303,8 @@ def test_tree_encode_device_vs_host(gpu):
         got, ends = _encode_device(torch, ents, out_shift=shift)
         assert got == want, shift
         assert ends == want_ends
+    for rs in (1, 4, 8):   # refs read bytewise when not 16-B aligned
+        assert _encode_device(torch, ents, out_shift=3, roots_shift=rs)[0] == want, rs
     with pytest.raises(N.GlfsxError):
         _encode_device(torch, ents, cap=len(want) - 1)
 
