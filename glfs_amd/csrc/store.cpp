@@ -221,6 +221,13 @@ uint64_t glfsx_store_stats(glfsx_store *s, uint64_t *posts, uint64_t *bytes,
   return s->blobs.size();
 }
 
-const char *glfsx_store_error(glfsx_store *s) { return s ? s->err.c_str() : "null store"; }
+// A copy per calling thread: concurrent Posts may replace s->err meanwhile.
+const char *glfsx_store_error(glfsx_store *s) {
+  if (!s) return "null store";
+  static thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(s->mu);
+  copy = s->err;
+  return copy.c_str();
+}
 
 }  // extern "C"

@@ -330,6 +330,8 @@ int glfsx_store_get(glfsx_store *s, const uint8_t cid[32], const void **data,
 /* number of distinct blobs; posts, bytes posted, posts re-hashed */
 uint64_t glfsx_store_stats(glfsx_store *s, uint64_t *posts, uint64_t *bytes,
                            uint64_t *hashed);
+/* The store's last error text; the pointer is valid on the calling thread
+ * until its next glfsx_store_error call. */
 const char *glfsx_store_error(glfsx_store *s);
 
 /* Batched getF decrypt from host memory (ref.go:113-126 over a tree level:
