@@ -968,18 +968,33 @@ __device__ __forceinline__ void wgt(bool chacha, int slot) {
 
 // A: ARX in the asm form (many waves per SIMD); false: the compiler's form,
 // which issues faster when a launch leaves a SIMD one or two waves
-template <int G, bool CHACHA, bool ALIGNED, int A = 2>
-__global__ __launch_bounds__(256) void k_pass(KArgs a) {
-  // one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext
-  // in the CHACHA pass, plaintext in the DEK pass): 40 KiB, 4 WGs per CU
-  constexpr int kStageU4 =
-      (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
-  __shared__ uint4 lds_u4[512 + kStageU4];
+// one LDS array: [0, 8 KiB) CV tree, then 4 waves x 8 KiB staging (ctext in
+// the CHACHA pass, plaintext in the DEK pass): 40 KiB, 4 WGs per CU
+template <bool CHACHA>
+constexpr int kStageOf = (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
+
+// DEK ready flags of a fused split launch (k_pass_dc): the DEK pass stores
+// message j's DEK with agent-scope atomic stores, waits for them, then sets
+// ready[j] = epoch; the CID workgroups of message j wait for that.
+__device__ __forceinline__ void publish_dek(uint8_t *dst, const uint32_t (&w)[8],
+                                            uint32_t *ready, uint32_t epoch) {
+  publish_cv(reinterpret_cast<uint32_t *>(dst), w);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(ready, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The body of one workgroup (number bid) of a pass.  FUSE: 0 = a pass of its
+// own; 1 = the DEK part of k_pass_dc (publishes each DEK with its ready
+// flag); 2 = the CID part (waits for its message's DEK).
+template <int G, bool CHACHA, bool ALIGNED, int A, int FUSE>
+__device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *lds_u4,
+                                          uint32_t *ready, uint32_t epoch) {
+  constexpr int kStageU4 = kStageOf<CHACHA>;
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
   WGT(0);
   // message j, sub-range sidx (split mode) = chunks [sidx*256G, +256G)
-  const uint64_t j = blockIdx.x >> a.split_log2;
-  const uint32_t sidx = blockIdx.x & ((1u << a.split_log2) - 1u);
+  const uint64_t j = bid >> a.split_log2;
+  const uint32_t sidx = bid & ((1u << a.split_log2) - 1u);
   const uint64_t len_full = (j + 1 == a.n) ? a.last_len : a.msg_len;
   constexpr uint64_t kSpan = uint64_t(256 * G) << 10;  // bytes per workgroup
   const uint64_t c0b = uint64_t(sidx) * kSpan;
@@ -996,7 +1011,26 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) key[i] = a.key[i];
   uint32_t dek[8];
-  if constexpr (CHACHA) {
+  if constexpr (FUSE == 2) {
+    // this message's DEK, from the DEK workgroups of the same launch: they
+    // were all dispatched before any CID workgroup, so they complete; the
+    // wait is bounded anyway (200 ms of s_memrealtime at 100 MHz)
+    if (t == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+             epoch) {
+        __builtin_amdgcn_s_sleep(4);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        lds[i] = load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dek[i] = __builtin_amdgcn_readfirstlane(lds[i]);
+    __syncthreads();
+  } else if constexpr (CHACHA) {
     // DEK written by the preceding pass into bytes [32,64) of this ref slot.
     const uint8_t *dp = ref + 32;
     if ((reinterpret_cast<uintptr_t>(dp) & 3) == 0) {
@@ -1038,7 +1072,10 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
                                      key, a.base, dek, cbase);
   }
   if (whole) {  // uniform: depends on len only; lane 0 holds the root output
-    if (t == 0) store_digest(ref + a.out_off, cv);
+    if (t == 0) {
+      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+      else store_digest(ref + a.out_off, cv);
+    }
     return;
   }
   const uint32_t active = (C + G - 1) / G;
@@ -1051,7 +1088,10 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   tree_reduce(lds, active, t, key, a.base, !split, cv);
   WGT(2);
   if (!split) {
-    if (t == 0) store_digest(ref + a.out_off, cv);
+    if (t == 0) {
+      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+      else store_digest(ref + a.out_off, cv);
+    }
     return;
   }
   // split (uniform): this workgroup's subtree CV to scratch; the message's
@@ -1084,10 +1124,33 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   __syncthreads();
   tree_reduce(lds, W, t, key, a.base, true, cv);
   if (t == 0) {
-    store_digest(ref + a.out_off, cv);
+    if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+    else store_digest(ref + a.out_off, cv);
     a.cnt[j] = 0;
   }
   WGT(3);
+}
+
+template <int G, bool CHACHA, bool ALIGNED, int A = 2>
+__global__ __launch_bounds__(256) void k_pass(KArgs a) {
+  __shared__ uint4 lds_u4[512 + kStageOf<CHACHA>];
+  pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr, 0u);
+}
+
+// Both passes of a split-mode post in one launch: workgroups [0, nd) run the
+// DEK pass (a), the rest the ChaCha20+CID pass (b), each CID workgroup
+// starting as soon as its message's DEK is published.  Workgroups are
+// dispatched in index order, so every DEK workgroup is resident or done
+// before the first CID workgroup waits; the CID pass fills the DEK pass's
+// tail instead of waiting for the whole launch to drain.
+template <int G>
+__global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, uint32_t nd,
+                                                 uint32_t *ready, uint32_t epoch) {
+  __shared__ uint4 lds_u4[512 + kStageOf<true>];
+  if (blockIdx.x < nd)
+    pass_body<G, false, true, 2, 1>(a, blockIdx.x, lds_u4, ready, epoch);
+  else
+    pass_body<G, true, true, 2, 2>(b, blockIdx.x - nd, lds_u4, ready, epoch);
 }
 
 // ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
@@ -1949,6 +2012,9 @@ struct ScratchSlot {
   size_t bytes;
   uint32_t *cnt;
   size_t cnt_words;
+  uint32_t *ready;     // k_pass_dc: per-message DEK ready flags (= epoch)
+  size_t ready_words;
+  uint32_t epoch;
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
@@ -1963,7 +2029,7 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) {
-    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0});
+    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0});
     sl = &g_scratch.back();
   }
   if (sl->bytes < bytes || sl->cnt_words < words) {
@@ -1995,6 +2061,40 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   }
   a->scratch = sl->p;
   a->cnt = sl->cnt;
+  return hipSuccess;
+}
+
+// k_pass_dc's ready flags for msgs messages on stream s, and this launch's
+// epoch (flags hold the epoch of the launch that set them, so they are never
+// reset; zero is never an epoch).
+hipError_t ready_get(uint64_t msgs, hipStream_t s, uint32_t **ready, uint32_t *epoch) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  ScratchSlot *sl = nullptr;
+  for (ScratchSlot &x : g_scratch)
+    if (x.dev == dev && x.stream == s) sl = &x;
+  if (!sl) return hipErrorInvalidValue;  // scratch_get first
+  if (sl->ready_words < msgs) {
+    if (sl->ready) {
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return e;
+      (void)hipFree(sl->ready);
+    }
+    sl->ready = nullptr;
+    sl->ready_words = 0;
+    const size_t want = std::max<size_t>(msgs, 4096);
+    e = hipMalloc(reinterpret_cast<void **>(&sl->ready), want * 4);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(sl->ready, 0, want * 4, s);
+    if (e != hipSuccess) return e;
+    sl->ready_words = want;
+    sl->epoch = 0;
+  }
+  if (++sl->epoch == 0) ++sl->epoch;
+  *ready = sl->ready;
+  *epoch = sl->epoch;
   return hipSuccess;
 }
 
@@ -2200,9 +2300,63 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
   return launch_pass<false>(a, maxlen, is_aligned(job), s);
 }
 
+// GLFSX_FUSED=0: split-mode posts as two launches (DEK pass, then CID pass)
+bool fused_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GLFSX_FUSED");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Split-mode post of many-wave size in one launch (k_pass_dc): both passes
+// of launch_keyed_hash + launch_cid_pass when each would be one k_pass<G,
+// CHACHA, true, 2> launch with the same plan.
+hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
+  *done = false;
+  if (!fused_enabled() || job.n < 2 || !is_aligned(job)) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(job.out.refs) | job.out.stride) & 3) return hipSuccess;
+  const uint64_t maxlen = std::max(job.msg_len, job.last_len);
+  int g;
+  uint32_t sl;
+  pass_plan(job.n, maxlen, &g, &sl);
+  const uint64_t wgs = job.n << sl;
+  if (sl == 0 || wgs <= latency_wgs() || (g != 1 && g != 2 && g != 4)) return hipSuccess;
+  const uint64_t chunks = job.n * ((maxlen + 1023) >> 10);
+  KArgs a = make_args(job);
+  for (int i = 0; i < 8; ++i) a.key[i] = job.salt[i];
+  a.base = kKeyed;
+  a.out_off = 32;
+  if (quad_ok(a, maxlen, true, sl) || chunks == 0) return hipSuccess;
+  a.split_log2 = sl;
+  hipError_t e = scratch_get(&a, 2 * wgs, 2 * job.n, s);
+  if (e != hipSuccess) return e;
+  uint32_t *ready;
+  uint32_t epoch;
+  e = ready_get(job.n, s, &ready, &epoch);
+  if (e != hipSuccess) return e;
+  KArgs b = a;
+  for (int i = 0; i < 8; ++i) b.key[i] = job.cid_key[i];
+  b.base = job.cid_keyed ? kKeyed : 0u;
+  b.out_off = 0;
+  b.scratch = a.scratch + wgs * 8;
+  b.cnt = a.cnt + job.n;
+  const dim3 grid(uint32_t(2 * wgs)), block(256);
+  switch (g) {
+    case 1: hipLaunchKernelGGL(k_pass_dc<1>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
+    case 2: hipLaunchKernelGGL(k_pass_dc<2>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
+    default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
+  }
+  *done = true;
+  return hipGetLastError();
+}
+
 hipError_t launch_post(const PostJob &job, hipStream_t s) {
   if (job.n == 0) return hipSuccess;
-  hipError_t e = launch_keyed_hash(job, 32, s);
+  bool done = false;
+  hipError_t e = launch_post_fused(job, s, &done);
+  if (e != hipSuccess || done) return e;
+  e = launch_keyed_hash(job, 32, s);
   if (e != hipSuccess) return e;
   return launch_cid_pass(job, s);
 }

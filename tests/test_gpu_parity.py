@@ -172,6 +172,35 @@ def test_arx_forms_vs_oracle(gpu, O, latency_wgs, split_target, bs, total):
         assert smalls[0][i] == want, i
 
 
+@pytest.mark.parametrize("bs,total", [(2 << 20, (37 << 20) + 123), (1 << 20, (70 << 20) + 1),
+                                      (300_000, 300_000 * 700 + 77), (4 << 20, 24 << 20)])
+def test_fused_split_post_vs_oracle(gpu, O, latency_wgs, split_target, bs, total):
+    """Split-mode posts of many workgroups run both passes in one launch
+    (k_pass_dc: DEK workgroups publish each message's DEK with a ready flag,
+    CID workgroups of the same launch wait for it).  Every ref and ctext
+    byte vs the oracle, keyed and unkeyed CIDs, at the default split target
+    and at maximal split (one chunk per lane), ragged last blocks, repeated
+    launches (the flags carry a per-launch epoch)."""
+    rng = random.Random(bs + total)
+    salt = bytes(rng.randrange(256) for _ in range(32))
+    data = O.fill_splitmix(total, total + 5)
+    latency_wgs(0)          # many-wave kernels even for small launches
+    n0 = (total + bs - 1) // bs
+    want = [O.post(salt, data[j * bs:(j + 1) * bs]) for j in range(n0)]
+    for target in (2048, 1 << 31, 2048):
+        split_target(target)
+        refs, ct = _post_batch_host(salt, data, bs)
+        for j, (r, c) in enumerate(want):
+            assert refs[64 * j:64 * j + 64] == r, (target, j)
+            assert ct[j * bs:j * bs + len(c)] == c, (target, j)
+    split_target(2048)
+    ck = bytes(range(32))
+    refs, _ = _post_batch_host(salt, data, bs, cid_key=ck)
+    for j in sorted({0, n0 - 1, rng.randrange(n0)}):
+        assert refs[64 * j:64 * j + 64] == O.post(salt, data[j * bs:(j + 1) * bs],
+                                                  cid_key=ck)[0], j
+
+
 @pytest.mark.parametrize("bs,total", [(1 << 20, (3 << 20) + 5), (1 << 20, 9 << 20),
                                       (2 << 20, (5 << 20) + 999), (5 << 20, 11 << 20),
                                       (300_000, 2_000_003), (65536, 65536 * 3 + 1),
