@@ -2321,7 +2321,12 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   uint32_t sl;
   pass_plan(job.n, maxlen, &g, &sl);
   const uint64_t wgs = job.n << sl;
-  if (sl == 0 || wgs <= latency_wgs() || (g != 1 && g != 2 && g != 4)) return hipSuccess;
+  // launches of 320-512 workgroups (default threshold) also run fused in the
+  // many-wave form: Create of 96 / 128 MiB at 1 MiB blocks (384 / 512
+  // workgroups) 359 -> 368 / 451 -> 487 GiB/s, 80 MiB a tie, 64 MiB (256)
+  // 6 % slower, so it stays in latency mode (scripts/lat_thr.py)
+  if (sl == 0 || wgs * 8 <= uint64_t(latency_wgs()) * 5 || (g != 1 && g != 2 && g != 4))
+    return hipSuccess;
   const uint64_t chunks = job.n * ((maxlen + 1023) >> 10);
   KArgs a = make_args(job);
   for (int i = 0; i < 8; ++i) a.key[i] = job.salt[i];
