@@ -64,6 +64,7 @@ SIGNATURES = {
     "glfsx_version": (_CP, []),
     "glfsx_set_split_target": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_set_latency_wgs": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "glfsx_debug_fused": (_U64, [ctypes.c_uint32, _U64]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),
     "glfsx_post": (_INT, [_CP, _VP, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP]),
@@ -77,6 +78,7 @@ SIGNATURES = {
     "glfsx_writer_write_device": (_INT, [_VP, _VP, _SZ, _VP]),
     "glfsx_writer_write_ctext": (_INT, [_VP, _VP, _U64, _U64, _VP]),
     "glfsx_writer_set_strict": (_INT, [_VP, _INT]),
+    "glfsx_writer_set_devices": (_INT, [_VP, _VP, _INT]),
     "glfsx_writer_error": (_CP, [_VP]),
     "glfsx_writer_finish": (_INT, [_VP, ctypes.POINTER(glfsx_root)]),
     "glfsx_writer_free": (None, [_VP]),
@@ -85,6 +87,9 @@ SIGNATURES = {
     "glfsx_create_device": (_INT, [_U64, _CP, _CP, _VP, _U64, _VP,
                                    ctypes.POINTER(glfsx_root),
                                    ctypes.POINTER(ctypes.c_uint64), _VP]),
+    "glfsx_create_devices": (_INT, [_U64, _CP, _CP, _INT, _VP, _VP, _VP, _VP, _VP,
+                                    ctypes.POINTER(glfsx_root),
+                                    ctypes.POINTER(ctypes.c_uint64)]),
     "glfsx_shard_device": (_INT, [_U64, _CP, _CP, _VP, _U64, _U64, _U64, _VP,
                                   _VP, _VP]),
     "glfsx_root_from_level1": (_INT, [_U64, _CP, _CP, _CP, _U64, _U64,

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
@@ -74,7 +75,7 @@ struct PinBuf {
     p = dp = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 4096);
-    HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p, want, hipHostMallocPortable));
     cap = want;
     HIP_TRY(hipHostGetDevicePointer(&dp, p, 0));
     return 0;
@@ -153,6 +154,39 @@ hipError_t stream_wait(hipStream_t s) {
   }
   g_spinners.fetch_sub(1, std::memory_order_relaxed);
   return e;
+}
+
+// One-launch split posts (k_pass_dc) report a failed DEK wait through a
+// word the host reads after the stream drains (fused_errors_take); the
+// calls that sync check it and repeat the work with two launches per post.
+// tls_fused = false while repeating; tls_fused_failed marks the failure.
+thread_local bool tls_fused = true;
+thread_local bool tls_fused_failed = false;
+
+int fused_check(hipStream_t s) {
+  if (const uint32_t v = fused_errors_take(s)) {
+    tls_fused_failed = true;
+    return fail(GLFSX_E_DEVICE,
+                "one-launch split post on stream %p: %s; its results were discarded",
+                static_cast<void *>(s),
+                v == 1 ? "a DEK wait timed out" : "work-item tickets out of range");
+  }
+  return 0;
+}
+
+// Run f(); if it failed because a one-launch split post failed, run it again
+// with two launches per post.
+template <class F>
+int with_fused_retry(F &&f) {
+  tls_fused_failed = false;
+  int rc = f();
+  if (rc && tls_fused_failed) {
+    tls_fused_failed = false;
+    tls_fused = false;
+    rc = f();
+    tls_fused = true;
+  }
+  return rc;
 }
 
 hipStream_t pick_stream(Ctx *c, void *stream) {
@@ -486,7 +520,7 @@ int post_level(Ctx *c, hipStream_t s, const uint8_t salt[32],
   j.out = out;
   words_from_key(j.salt, salt);
   cid_words(j, cid_key);
-  HIP_TRY(launch_post(j, s));
+  HIP_TRY(launch_post(j, s, tls_fused));
   return 0;
 }
 
@@ -506,7 +540,7 @@ int build_up(Ctx *c, hipStream_t s, const Salts &salts, const uint8_t *cid_key,
       *posts += 1;
       HIP_TRY(hipMemcpyAsync(root_ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
       HIP_TRY(stream_wait(s));
-      return 0;
+      return fused_check(s);
     }
     const uint64_t m = (nodes + bf - 1) / bf;
     if (int e = spare->ensure(m * bs)) return e;
@@ -539,6 +573,8 @@ struct WSlot {
   hipEvent_t up = nullptr, hashed = nullptr, done = nullptr;
   uint64_t nblk = 0;  // blocks in flight
   uint64_t seq = 0;   // submission order
+  PostJob job{};      // the batch's post (repeated if its fused launch failed)
+  int lane = 0;       // writer lane (device + streams) the batch runs on
   bool busy = false;
   bool on_dev = false;  // the staged bytes [0, used) live in d_in, not h_in
                         // (written by glfsx_writer_write_device)
@@ -577,6 +613,96 @@ void release_slot(WSlot &sl) {
   sl = WSlot();
 }
 
+// A writer lane: one device with its upload, hash and download streams.
+// Batches go round-robin over the lanes (glfsx_writer_set_devices), so one
+// Writer fed from one host stream hashes on several GPUs at once, each over
+// its own PCIe link, while the Posts still replay in block order.
+struct WLane {
+  int dev = 0;
+  hipStream_t ws = nullptr, s_up = nullptr, s_down = nullptr;
+  bool own = false;  // streams of its own (not the writer's home streams)
+};
+
+// Pooled writer resources.  take_slot / give_slot_locked / *_locked run
+// with g_pool_mu held.
+void take_slot(WSlot &x, int dev, int lane) {
+  for (size_t i = g_slot_pool.size(); i-- > 0;) {
+    if (g_slot_pool[i].dev == dev) {
+      x = g_slot_pool[i];
+      g_slot_pool.erase(g_slot_pool.begin() + i);
+      break;
+    }
+  }
+  x.dev = dev;
+  x.lane = lane;
+}
+
+void give_slot_locked(WSlot &sl) {
+  sl.busy = false;
+  sl.nblk = 0;
+  sl.on_dev = false;
+  if (sl.dev >= 0 && g_slot_pool.size() < 64 * 4)
+    g_slot_pool.push_back(sl);  // buffers are reused by the next writer
+  else
+    release_slot(sl);
+  sl = WSlot();
+}
+
+int current_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
+
+// A lane's streams of its own: from the pool, or new ones on its device.
+int take_streams(WLane &L) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = g_stream_pool.size(); i-- > 0;) {
+      if (g_stream_pool[i].dev == L.dev) {
+        L.s_up = g_stream_pool[i].up;
+        L.ws = g_stream_pool[i].hash;
+        L.s_down = g_stream_pool[i].down;
+        g_stream_pool.erase(g_stream_pool.begin() + i);
+        L.own = true;
+        return 0;
+      }
+    }
+  }
+  const int home = current_device();
+  HIP_TRY(hipSetDevice(L.dev));
+  hipError_t e = hipStreamCreateWithFlags(&L.ws, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.s_up, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.s_down, hipStreamNonBlocking);
+  (void)hipSetDevice(home);
+  if (e != hipSuccess) return fail(GLFSX_E_DEVICE, "hipStreamCreate on device %d failed", L.dev);
+  L.own = true;
+  return 0;
+}
+
+void give_streams_locked(WLane &L) {
+  if (!L.own) return;
+  L.own = false;
+  if (g_stream_pool.size() < 64) {
+    g_stream_pool.push_back({L.dev, L.s_up, L.ws, L.s_down});
+    return;
+  }
+  const int home = current_device();
+  (void)hipSetDevice(L.dev);
+  for (hipStream_t st : {L.s_up, L.ws, L.s_down})
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      release_stream_scratch(st);
+      (void)hipStreamDestroy(st);
+    }
+  (void)hipSetDevice(home);
+}
+
+void give_streams(WLane &L) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  give_streams_locked(L);
+}
+
 // Batch slots: one being filled, one uploading/hashing, one downloading.
 // GLFSX_SLOTS (2..4) and GLFSX_BATCH_MIB override the defaults (tuning).
 constexpr int kMaxSlots = 4;
@@ -587,7 +713,7 @@ constexpr int kMaxSlots = 4;
 // single-goroutine (blob.go:71-83), but a goroutine may run on any OS thread
 // between cgo calls.
 struct glfsx_writer {
-  int dev = 0;
+  int dev = 0;  // home device: single posts (index nodes, tail) and device input
   // batch streams: uploads, kernels (also the single posts), downloads, so
   // batch k+1's H2D overlaps batch k's D2H on the full-duplex link
   hipStream_t ws = nullptr, s_up = nullptr, s_down = nullptr;
@@ -606,8 +732,9 @@ struct glfsx_writer {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   PinBuf h_ctx;
   DevBuf d_ctx, d_ptx, d_rfx;
-  WSlot slot[kMaxSlots];
-  int nslots = 3;
+  std::vector<WLane> lanes;  // lane 0 = the home device and streams by default
+  std::vector<WSlot> slot;   // a ring: slot i runs on lane i % lanes.size()
+  int nslots = 3;            // slots per lane
   int cur = 0;               // slot being filled
   uint64_t seq = 0;
   uint64_t batch_blocks = 1;
@@ -625,12 +752,25 @@ const uint8_t *cidk(const glfsx_writer *w) {
   return w->has_cid_key ? w->cid_key : nullptr;
 }
 
+// Make `dev` current for a scope and `home` current again at its end (a
+// writer's lanes may live on other devices than its home).
+struct DevScope {
+  int home;
+  bool moved;
+  DevScope(int dev, int home_) : home(home_), moved(dev != home_) {
+    if (moved) (void)hipSetDevice(dev);
+  }
+  ~DevScope() {
+    if (moved) (void)hipSetDevice(home);
+  }
+};
+
 // Grow a pinned buffer keeping its first `keep` bytes.
 int pin_grow(PinBuf &b, size_t need, size_t keep) {
   if (need <= b.cap) return 0;
   size_t want = std::max(need, b.cap * 2);
   void *p = nullptr;
-  HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(&p, want, hipHostMallocPortable));
   void *dp = nullptr;
   if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
     (void)hipHostFree(p);
@@ -769,7 +909,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
   j.out = RefLayout{o.d_ref.u8(), ~0ull, 0};
   words_from_key(j.salt, salt);
   cid_words(j, cidk(w));
-  HIP_TRY(launch_post(j, w->ws));
+  HIP_TRY(launch_post(j, w->ws, tls_fused));
   if (n)
     HIP_TRY(hipMemcpyAsync(o.h_ct.p, o.d_ct.p, n, hipMemcpyDeviceToHost, w->ws));
   HIP_TRY(hipMemcpyAsync(o.h_ref.p, o.d_ref.p, 64, hipMemcpyDeviceToHost, w->ws));
@@ -813,12 +953,47 @@ int add_ref(glfsx_writer *w, size_t i, const uint8_t ref[64]) {
   return add_ref(w, i + 1, r2);
 }
 
+// A one-launch split post on the hash stream failed (fused_check): the
+// error word cannot tell which batch's launch it was, so every batch still
+// in flight is hashed again with two launches per post, in order.
+int rehash_inflight(glfsx_writer *w) {
+  for (const WLane &L : w->lanes) {
+    DevScope d(L.dev, w->dev);
+    HIP_TRY(hipStreamSynchronize(L.ws));
+    HIP_TRY(hipStreamSynchronize(L.s_down));
+    (void)fused_errors_take(L.ws);
+  }
+  for (WSlot &x : w->slot) {
+    if (!x.busy) continue;
+    const WLane &L = w->lanes[x.lane];
+    DevScope d(L.dev, w->dev);
+    HIP_TRY(launch_post(x.job, L.ws, false));
+    HIP_TRY(hipMemcpyAsync(x.h_refs.p, x.d_refs.p, x.nblk * 64, hipMemcpyDeviceToHost, L.ws));
+    if (w->post)
+      HIP_TRY(hipMemcpyAsync(x.h_ct.p, x.d_ct.p, x.nblk * w->bs, hipMemcpyDeviceToHost,
+                             L.ws));
+  }
+  for (const WLane &L : w->lanes) {
+    DevScope d(L.dev, w->dev);
+    HIP_TRY(stream_wait(L.ws));
+  }
+  return 0;
+}
+
 // Wait for an in-flight batch and replay postBuf (blob.go:152-163) for each
 // of its blocks, in order.
 int complete(glfsx_writer *w, WSlot &sl) {
   if (!sl.busy) return 0;
-  sl.busy = false;
   HIP_TRY(hipEventSynchronize(sl.done));
+  bool failed;
+  {
+    const WLane &L = w->lanes[sl.lane];
+    DevScope d(L.dev, w->dev);
+    failed = fused_errors_take(L.ws) != 0;
+  }
+  if (failed)
+    if (int e = rehash_inflight(w)) return e;
+  sl.busy = false;
   for (uint64_t b = 0; b < sl.nblk; ++b) {
     const uint8_t *ref = sl.h_refs.u8() + 64 * b;
     if (w->post) {
@@ -837,8 +1012,10 @@ int complete(glfsx_writer *w, WSlot &sl) {
 int submit(glfsx_writer *w) {
   if (w->full == 0) return 0;
   WSlot &sl = w->slot[w->cur];
-  const int next = (w->cur + 1) % w->nslots;
+  const int next = (w->cur + 1) % int(w->slot.size());
   WSlot &nx = w->slot[next];
+  const WLane &L = w->lanes[sl.lane];
+  DevScope dscope(L.dev, w->dev);
   const uint64_t nbytes = w->full * w->bs;
   if (int e = sl.d_in.ensure(nbytes)) return e;
   if (int e = sl.d_ct.ensure(nbytes)) return e;
@@ -852,9 +1029,9 @@ int submit(glfsx_writer *w) {
     HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
   }
   if (!sl.on_dev)  // device-written bytes are already in d_in (s_up order)
-    HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, w->s_up));
-  HIP_TRY(hipEventRecord(sl.up, w->s_up));
-  HIP_TRY(hipStreamWaitEvent(w->ws, sl.up, 0));
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, sl.h_in.p, nbytes, hipMemcpyHostToDevice, L.s_up));
+  HIP_TRY(hipEventRecord(sl.up, L.s_up));
+  HIP_TRY(hipStreamWaitEvent(L.ws, sl.up, 0));
   PostJob j{};
   j.src = sl.d_in.u8();
   j.ctext = sl.d_ct.u8();
@@ -865,26 +1042,27 @@ int submit(glfsx_writer *w) {
   j.out = RefLayout{sl.d_refs.u8(), ~0ull, 0};
   words_from_key(j.salt, w->salts.raw);
   cid_words(j, cidk(w));
-  HIP_TRY(launch_post(j, w->ws));
-  HIP_TRY(hipEventRecord(sl.hashed, w->ws));
-  HIP_TRY(hipStreamWaitEvent(w->s_down, sl.hashed, 0));
+  sl.job = j;
+  HIP_TRY(launch_post(j, L.ws, tls_fused));
+  HIP_TRY(hipEventRecord(sl.hashed, L.ws));
+  HIP_TRY(hipStreamWaitEvent(L.s_down, sl.hashed, 0));
   HIP_TRY(hipMemcpyAsync(sl.h_refs.p, sl.d_refs.p, w->full * 64,
-                         hipMemcpyDeviceToHost, w->s_down));
+                         hipMemcpyDeviceToHost, L.s_down));
   if (w->post)
     HIP_TRY(hipMemcpyAsync(sl.h_ct.p, sl.d_ct.p, nbytes, hipMemcpyDeviceToHost,
-                           w->s_down));
-  HIP_TRY(hipEventRecord(sl.done, w->s_down));
+                           L.s_down));
+  HIP_TRY(hipEventRecord(sl.done, L.s_down));
   sl.nblk = w->full;
   sl.seq = ++w->seq;
   sl.busy = true;
   // `nx` is the oldest batch in flight (submitted nslots-1 batches ago):
   // completing it keeps Posts in order
   if (int e = complete(w, nx)) return e;
-  if (sl.on_dev) {  // carry the partial block over on the device
+  if (sl.on_dev) {  // carry the partial block over on the device (one lane)
     if (int e = nx.d_in.ensure(w->batch_blocks * w->bs + 64)) return e;
     if (w->partial)
       HIP_TRY(hipMemcpyAsync(nx.d_in.p, sl.d_in.u8() + nbytes, w->partial,
-                             hipMemcpyDeviceToDevice, w->s_up));
+                             hipMemcpyDeviceToDevice, L.s_up));
     nx.on_dev = true;
   } else {
     if (int e = pin_grow(nx.h_in, std::max<uint64_t>(w->partial, 1), 0)) return e;
@@ -972,6 +1150,11 @@ const char *glfsx_version(void) { return "glfsx 0.1 gfx950"; }
 uint32_t glfsx_set_split_target(uint32_t wgs) { return set_split_target(wgs); }
 uint32_t glfsx_set_latency_wgs(uint32_t wgs) { return set_latency_wgs(wgs); }
 
+uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us) {
+  fused_debug(skip_msg, wait_us);
+  return fused_timeouts();
+}
+
 #if GLFSX_WGTIME
 // diagnostic builds only (tools/build_variant.sh): the bulk passes' phase
 // timestamps, 8192 x 8 words
@@ -1030,7 +1213,7 @@ int glfsx_post_batch_device(const uint8_t salt[32], const void *d_ptext,
   j.out = RefLayout{static_cast<uint8_t *>(d_refs), ~0ull, 0};
   words_from_key(j.salt, salt);
   cid_words(j, cid_key);
-  HIP_TRY(launch_post(j, pick_stream(c, stream)));
+  HIP_TRY(launch_post(j, pick_stream(c, stream), false));
   return 0;
 }
 
@@ -1118,7 +1301,7 @@ int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
   j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
   words_from_key(j.salt, salt);
   cid_words(j, cid_key);
-  HIP_TRY(launch_post(j, c->stream));
+  HIP_TRY(launch_post(j, c->stream, tls_fused));
   HIP_TRY(hipMemcpyAsync(ref_out, c->d_refs.p, 64, hipMemcpyDeviceToHost, c->stream));
   if (ctext_out && n)
     HIP_TRY(hipMemcpyAsync(ctext_out, c->d_ct.p, n, hipMemcpyDeviceToHost, c->stream));
@@ -1160,13 +1343,16 @@ int glfsx_post_batch(const uint8_t salt[32], const void *ptext, uint64_t total,
     j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
     words_from_key(j.salt, salt);
     cid_words(j, cid_key);
-    HIP_TRY(launch_post(j, c->stream));
-    HIP_TRY(hipMemcpyAsync(refs_out + 64 * b0, c->d_refs.p, nb * 64,
-                           hipMemcpyDeviceToHost, c->stream));
-    if (ctext_out)
-      HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(ctext_out) + off, c->d_ct.p,
-                             bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(stream_wait(c->stream));
+    for (bool fused : {true, false}) {  // again with two launches if the fused one failed
+      HIP_TRY(launch_post(j, c->stream, fused));
+      HIP_TRY(hipMemcpyAsync(refs_out + 64 * b0, c->d_refs.p, nb * 64,
+                             hipMemcpyDeviceToHost, c->stream));
+      if (ctext_out)
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(ctext_out) + off, c->d_ct.p,
+                               bytes, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(stream_wait(c->stream));
+      if (!fused_errors_take(c->stream)) break;
+    }
   }
   return 0;
 }
@@ -1213,18 +1399,10 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
   if (const char *e = getenv("GLFSX_BATCH_MIB")) batch_mib = std::max(1ull, strtoull(e, nullptr, 10));
   if (const char *e = getenv("GLFSX_SLOTS")) w->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
   w->batch_blocks = std::max<uint64_t>(1, (batch_mib << 20) / bs);
+  w->slot.resize(w->nslots);
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (int k = 0; k < w->nslots; ++k) {
-      for (size_t i = g_slot_pool.size(); i-- > 0;) {
-        if (g_slot_pool[i].dev == w->dev) {
-          w->slot[k] = g_slot_pool[i];
-          g_slot_pool.erase(g_slot_pool.begin() + i);
-          break;
-        }
-      }
-      w->slot[k].dev = w->dev;
-    }
+    for (WSlot &x : w->slot) take_slot(x, w->dev, 0);
     for (size_t i = g_one_pool.size(); i-- > 0;) {
       if (g_one_pool[i].dev == w->dev) {
         w->one = g_one_pool[i];
@@ -1251,8 +1429,41 @@ glfsx_writer *glfsx_writer_new(uint64_t block_size, uint64_t store_max,
     *err = fail(GLFSX_E_DEVICE, "hipStreamCreate failed");
     return nullptr;
   }
+  w->lanes.push_back(WLane{w->dev, w->ws, w->s_up, w->s_down, false});
   *err = 0;
   return w;
+}
+
+int glfsx_writer_set_devices(glfsx_writer *w, const int *devs, int ndev) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  if (!devs || ndev < 1 || ndev > 64) return fail(GLFSX_E_ARG, "need 1..64 devices");
+  if (w->seq || w->full || w->partial || w->size || w->sticky || w->ev_in)
+    return fail(GLFSX_E_ARG, "glfsx_writer_set_devices: the writer has already been written to");
+  const int n = glfsx_device_count();
+  for (int k = 0; k < ndev; ++k)
+    if (devs[k] < 0 || devs[k] >= n)
+      return fail(GLFSX_E_ARG, "device %d out of range (%d devices)", devs[k], n);
+  std::vector<WLane> lanes(ndev);
+  for (int k = 0; k < ndev; ++k) {
+    lanes[k].dev = devs[k];
+    if (k == 0 && devs[0] == w->dev) {  // the home streams
+      lanes[0] = WLane{w->dev, w->ws, w->s_up, w->s_down, false};
+      continue;
+    }
+    if (int e = take_streams(lanes[k])) {
+      for (int i = 0; i < k; ++i) give_streams(lanes[i]);
+      return e;
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (WLane &L : w->lanes) give_streams_locked(L);
+  for (WSlot &x : w->slot) give_slot_locked(x);
+  w->lanes = std::move(lanes);
+  w->slot.assign(size_t(w->nslots) * ndev, WSlot());
+  for (size_t i = 0; i < w->slot.size(); ++i)
+    take_slot(w->slot[i], w->lanes[i % ndev].dev, int(i % ndev));
+  w->cur = 0;
+  return 0;
 }
 
 namespace {
@@ -1378,6 +1589,8 @@ int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
   if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
   if (n && !d_data) return call.done(fail(GLFSX_E_ARG, "null data"));
   if (n == 0) return 0;
+  if (w->lanes.size() != 1)
+    return call.done(fail(GLFSX_E_UNSUPPORTED, "device input needs a one-device writer"));
   hipStream_t cs = static_cast<hipStream_t>(stream);
   auto go = [&]() -> int {
     if (!w->ev_in) {
@@ -1410,6 +1623,8 @@ int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
   if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
   if (total == 0) return 0;
   if (!ctext || !refs) return call.done(fail(GLFSX_E_ARG, "null argument"));
+  if (w->lanes.size() != 1)
+    return call.done(fail(GLFSX_E_UNSUPPORTED, "device input needs a one-device writer"));
   if (block_size == 0 || block_size % 64)
     return call.done(fail(GLFSX_E_UNSUPPORTED, "decrypt needs block_size %% 64 == 0"));
   auto go = [&]() -> int {
@@ -1488,21 +1703,20 @@ void glfsx_writer_free(glfsx_writer *w) {
   (void)hipSetDevice(w->dev);
   // a writer that never submitted a batch nor took device input, and did
   // not fail, has nothing in flight (its single posts waited for themselves)
-  if (w->seq || w->ev_in || w->sticky)
+  if (w->seq || w->ev_in || w->sticky) {
     for (hipStream_t st : {w->s_up, w->ws, w->s_down})
       if (st) (void)hipStreamSynchronize(st);
+    for (const WLane &L : w->lanes)
+      if (L.own) {
+        DevScope d(L.dev, w->dev);
+        for (hipStream_t st : {L.s_up, L.ws, L.s_down}) (void)hipStreamSynchronize(st);
+      }
+  }
   std::vector<hipStream_t> drop;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (auto &sl : w->slot) {
-      sl.busy = false;
-      sl.nblk = 0;
-      sl.on_dev = false;
-      if (sl.dev >= 0 && g_slot_pool.size() < 16 * kMaxSlots)
-        g_slot_pool.push_back(sl);  // buffers are reused by the next writer
-      else
-        release_slot(sl);
-    }
+    for (auto &sl : w->slot) give_slot_locked(sl);
+    for (WLane &L : w->lanes) give_streams_locked(L);
     if (g_one_pool.size() < 16) {
       g_one_pool.push_back(w->one);
     } else {
@@ -1512,7 +1726,7 @@ void glfsx_writer_free(glfsx_writer *w) {
       for (void *p : {o.h_ct.p, o.h_ref.p})
         if (p) (void)hipHostFree(p);
     }
-    if (w->ws && g_stream_pool.size() < 16)
+    if (w->ws && g_stream_pool.size() < 64)
       g_stream_pool.push_back({w->dev, w->s_up, w->ws, w->s_down});
     else
       drop = {w->s_up, w->ws, w->s_down};
@@ -1543,10 +1757,208 @@ int glfsx_create(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
   return e;
 }
 
+namespace {
+int create_device_impl(uint64_t block_size, const uint8_t *salt,
+                       const uint8_t *cid_key, const void *d_data,
+                       uint64_t size, void *d_ctext, glfsx_root *out,
+                       uint64_t *n_posts, void *stream);
+int shard_device_impl(uint64_t block_size, const uint8_t *salt,
+                      const uint8_t *cid_key, const void *d_range,
+                      uint64_t size, uint64_t first_block, uint64_t nb,
+                      void *d_ctext, uint8_t *level1_out, void *stream);
+int root_from_level1_impl(uint64_t block_size, const uint8_t *salt,
+                          const uint8_t *cid_key, const uint8_t *level1,
+                          uint64_t n1, uint64_t size, glfsx_root *out);
+}  // namespace
+
 int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
                         const uint8_t *cid_key, const void *d_data,
                         uint64_t size, void *d_ctext, glfsx_root *out,
                         uint64_t *n_posts, void *stream) {
+  return with_fused_retry([&] {
+    return create_device_impl(block_size, salt, cid_key, d_data, size, d_ctext, out,
+                              n_posts, stream);
+  });
+}
+
+int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
+                       const uint8_t *cid_key, const void *d_range,
+                       uint64_t size, uint64_t first_block, uint64_t nb,
+                       void *d_ctext, uint8_t *level1_out, void *stream) {
+  return with_fused_retry([&] {
+    return shard_device_impl(block_size, salt, cid_key, d_range, size, first_block, nb,
+                             d_ctext, level1_out, stream);
+  });
+}
+
+int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
+                           const uint8_t *cid_key, const uint8_t *level1,
+                           uint64_t n1, uint64_t size, glfsx_root *out) {
+  return with_fused_retry([&] {
+    return root_from_level1_impl(block_size, salt, cid_key, level1, n1, size, out);
+  });
+}
+
+namespace {
+// Persistent worker threads of glfsx_create_devices, one per (device,
+// index): part k of a call runs on the worker of its device whose index
+// counts the earlier parts on the same device.  A worker keeps its thread's
+// context (stream, level buffers, scratch) across calls, so a call creates
+// no streams or buffers once warm.  Calls are serialised (each takes every
+// device it names).
+struct PartWorker {
+  int dev = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<int()> fn;
+  bool pending = false, done = false;
+  int rc = 0;
+  std::string err;
+  void loop() {
+    tls_dev = dev;
+    for (;;) {
+      std::function<int()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return pending; });
+        f = std::move(fn);
+        pending = false;
+      }
+      const int r = f();
+      std::string e = r ? tls_err : std::string();
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        rc = r;
+        err = std::move(e);
+        done = true;
+      }
+      cv.notify_all();
+    }
+  }
+  void submit(std::function<int()> f) {
+    std::lock_guard<std::mutex> lk(mu);
+    fn = std::move(f);
+    done = false;
+    pending = true;
+    cv.notify_all();
+  }
+  int wait(std::string *e) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+    *e = err;
+    return rc;
+  }
+};
+std::mutex g_parts_mu;  // one glfsx_create_devices call at a time
+std::vector<std::pair<std::pair<int, int>, PartWorker *>> g_part_workers;
+
+PartWorker *part_worker(int dev, int idx) {
+  for (auto &x : g_part_workers)
+    if (x.first == std::make_pair(dev, idx)) return x.second;
+  auto *pw = new PartWorker();  // lives for the process, like its thread
+  pw->dev = dev;
+  std::thread([pw] { pw->loop(); }).detach();
+  g_part_workers.push_back({{dev, idx}, pw});
+  return pw;
+}
+
+// Run fns[k] on the worker of (devs[k], its index); the first failure (in
+// part order) is returned with its text.
+int run_parts(const int *devs, std::vector<std::function<int()>> &fns) {
+  std::vector<PartWorker *> ws(fns.size());
+  for (size_t k = 0; k < fns.size(); ++k) {
+    int idx = 0;
+    for (size_t i = 0; i < k; ++i) idx += devs[i] == devs[k];
+    ws[k] = part_worker(devs[k], idx);
+  }
+  for (size_t k = 0; k < fns.size(); ++k) ws[k]->submit(std::move(fns[k]));
+  int first = 0;
+  std::string msg;
+  for (size_t k = 0; k < fns.size(); ++k) {
+    std::string e;
+    const int rc = ws[k]->wait(&e);
+    if (rc && !first) {
+      first = rc;
+      msg = "part " + std::to_string(k) + " (device " + std::to_string(devs[k]) + "): " + e;
+    }
+  }
+  return first ? fail(first, "%s", msg.c_str()) : 0;
+}
+}  // namespace
+
+// Create over a blob whose bytes lie on several devices (in one
+// process): part k = bytes of blocks [first_k, first_k + nb_k) on devs[k];
+// each device posts its data blocks and level-1 nodes concurrently, the
+// level-1 refs are gathered on the host and levels >= 2 posted on devs[0].
+int glfsx_create_devices(uint64_t block_size, const uint8_t *salt,
+                         const uint8_t *cid_key, int nparts, const int *devs,
+                         const void *const *d_parts, const uint64_t *part_sizes,
+                         void *const *d_ctexts, uint8_t *level1_out,
+                         glfsx_root *out, uint64_t *n_posts) {
+  if (!out || !devs || !d_parts || !part_sizes || nparts < 1 || nparts > 1024)
+    return fail(GLFSX_E_ARG, "bad arguments");
+  if (int e = check_block_size(block_size)) return e;
+  const int ndev = glfsx_device_count();
+  const uint64_t bs = block_size, bf = bs / 64, span = bs * bf;
+  uint64_t size = 0;
+  for (int k = 0; k < nparts; ++k) {
+    if (devs[k] < 0 || devs[k] >= ndev)
+      return fail(GLFSX_E_ARG, "device %d out of range (%d devices)", devs[k], ndev);
+    if (part_sizes[k] && !d_parts[k]) return fail(GLFSX_E_ARG, "null part %d", k);
+    if (k + 1 < nparts && (part_sizes[k] == 0 || part_sizes[k] % span))
+      return fail(GLFSX_E_ARG,
+                  "part %d: %llu bytes; every part but the last must be a positive "
+                  "multiple of block_size * block_size/64 = %llu (whole level-1 nodes)",
+                  k, (unsigned long long)part_sizes[k], (unsigned long long)span);
+    size += part_sizes[k];
+  }
+  if (nparts > 1 && part_sizes[nparts - 1] == 0)
+    return fail(GLFSX_E_ARG, "the last part is empty");
+  std::lock_guard<std::mutex> lk(g_parts_mu);
+  const uint64_t n0 = (size + bs - 1) / bs;
+  if (nparts == 1 || n0 <= bf) {  // one part: Create on its device
+    std::vector<std::function<int()>> fns{[&] {
+      return glfsx_create_device(bs, salt, cid_key, d_parts[0], size,
+                                 d_ctexts ? d_ctexts[0] : nullptr, out, n_posts, nullptr);
+    }};
+    return run_parts(devs, fns);  // level1_out is not written
+  }
+  const uint64_t n1 = (n0 + bf - 1) / bf;
+  std::vector<uint8_t> lvl1(n1 * 64);
+  std::vector<std::function<int()>> fns;
+  uint64_t first = 0;
+  for (int k = 0; k < nparts; ++k) {
+    const uint64_t nb = (part_sizes[k] + bs - 1) / bs;
+    uint8_t *dst = lvl1.data() + (first / bf) * 64;
+    void *ct = d_ctexts ? d_ctexts[k] : nullptr;
+    const void *src = d_parts[k];
+    fns.push_back([=] {
+      return glfsx_shard_device(bs, salt, cid_key, src, size, first, nb, ct, dst, nullptr);
+    });
+    first += nb;
+  }
+  if (int e = run_parts(devs, fns)) return e;
+  std::vector<std::function<int()>> top{[&] {
+    return glfsx_root_from_level1(bs, salt, cid_key, lvl1.data(), n1, size, out);
+  }};
+  if (int e = run_parts(devs, top)) return e;
+  if (level1_out) memcpy(level1_out, lvl1.data(), lvl1.size());
+  if (n_posts) {
+    uint64_t posts = n0 + n1;
+    for (uint64_t r = n1; r > 1;) {
+      r = (r + bf - 1) / bf;
+      posts += r;
+    }
+    *n_posts = posts;
+  }
+  return 0;
+}
+
+namespace {
+int create_device_impl(uint64_t block_size, const uint8_t *salt,
+                       const uint8_t *cid_key, const void *d_data,
+                       uint64_t size, void *d_ctext, glfsx_root *out,
+                       uint64_t *n_posts, void *stream) {
   if (!out || (size && !d_data)) return fail(GLFSX_E_ARG, "null argument");
   if (int e = check_block_size(block_size)) return e;
   Ctx *c;
@@ -1572,7 +1984,7 @@ int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
     j.out = RefLayout{c->d_refs.u8(), ~0ull, 0};
     words_from_key(j.salt, n0 ? salts.raw : salts.index);
     cid_words(j, cid_key);
-    HIP_TRY(launch_post(j, s));
+    HIP_TRY(launch_post(j, s, tls_fused));
     HIP_TRY(hipMemcpyAsync(out->ref, c->d_refs.p, 64, hipMemcpyDeviceToHost, s));
     HIP_TRY(stream_wait(s));
     posts = 1;
@@ -1590,7 +2002,7 @@ int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
     j.out = RefLayout{c->d_lvl_a.u8(), bf, bs};
     words_from_key(j.salt, salts.raw);
     cid_words(j, cid_key);
-    HIP_TRY(launch_post(j, s));
+    HIP_TRY(launch_post(j, s, tls_fused));
     posts = n0;
     if (int e = build_up(c, s, salts, cid_key, bs, c->d_lvl_a.u8(), n1,
                          &c->d_lvl_b, out->ref, &posts))
@@ -1602,10 +2014,10 @@ int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
   return 0;
 }
 
-int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
-                       const uint8_t *cid_key, const void *d_range,
-                       uint64_t size, uint64_t first_block, uint64_t nb,
-                       void *d_ctext, uint8_t *level1_out, void *stream) {
+int shard_device_impl(uint64_t block_size, const uint8_t *salt,
+                      const uint8_t *cid_key, const void *d_range,
+                      uint64_t size, uint64_t first_block, uint64_t nb,
+                      void *d_ctext, uint8_t *level1_out, void *stream) {
   if (!level1_out || (nb && !d_range)) return fail(GLFSX_E_ARG, "null argument");
   if (int e = check_block_size(block_size)) return e;
   const uint64_t bs = block_size, bf = bs / 64;
@@ -1636,18 +2048,18 @@ int glfsx_shard_device(uint64_t block_size, const uint8_t *salt,
   j.out = RefLayout{c->d_lvl_a.u8(), bf, bs};
   words_from_key(j.salt, salts.raw);
   cid_words(j, cid_key);
-  HIP_TRY(launch_post(j, s));
+  HIP_TRY(launch_post(j, s, tls_fused));
   if (int e = post_level(c, s, salts.index, cid_key, c->d_lvl_a.u8(), m, bs,
                          c->d_ct.u8(), RefLayout{c->d_refs.u8(), ~0ull, 0}))
     return e;
   HIP_TRY(hipMemcpyAsync(level1_out, c->d_refs.p, m * 64, hipMemcpyDeviceToHost, s));
   HIP_TRY(stream_wait(s));
-  return 0;
+  return fused_check(s);
 }
 
-int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
-                           const uint8_t *cid_key, const uint8_t *level1,
-                           uint64_t n1, uint64_t size, glfsx_root *out) {
+int root_from_level1_impl(uint64_t block_size, const uint8_t *salt,
+                          const uint8_t *cid_key, const uint8_t *level1,
+                          uint64_t n1, uint64_t size, glfsx_root *out) {
   if (!level1 || !out || n1 == 0) return fail(GLFSX_E_ARG, "null argument");
   if (int e = check_block_size(block_size)) return e;
   const uint64_t bs = block_size, bf = bs / 64;
@@ -1678,6 +2090,8 @@ int glfsx_root_from_level1(uint64_t block_size, const uint8_t *salt,
   return build_up(c, c->stream, salts, cid_key, bs, c->d_lvl_a.u8(), m,
                   &c->d_lvl_b, out->ref, &posts);
 }
+}  // namespace
+
 
 int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,
                        uint64_t n) {
@@ -1752,7 +2166,7 @@ int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
       pj.out = RefLayout{ref, ~0ull, 0};
       words_from_key(pj.salt, salts.raw);
       cid_words(pj, cid_key);
-      HIP_TRY(launch_post(pj, s));
+      HIP_TRY(launch_post(pj, s, tls_fused));
     } else {
       glfsx_root r;
       if (int e = glfsx_create_device(block_size, salt, cid_key, src, lens[i], ct, &r,

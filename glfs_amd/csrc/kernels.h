@@ -35,7 +35,20 @@ struct PostJob {
 // 256 workgroups x 256 lanes x 64 BLAKE3 chunks (split mode, 4 GiB).
 constexpr uint64_t kMaxMsgLen = 256ull * 256 * 64 * 1024;
 
-hipError_t launch_post(const PostJob &job, hipStream_t s);
+// fused = false: never the one-launch split form (k_pass_dc), for callers
+// that return before the stream is synchronised (its failure is only
+// visible to fused_errors_take after the stream has drained).
+hipError_t launch_post(const PostJob &job, hipStream_t s, bool fused = true);
+
+// After stream s has drained: nonzero when a one-launch split post on it
+// gave up waiting for a DEK since the last call (its refs and ctext are
+// invalid; the caller fails or repeats the post with fused = false).
+uint32_t fused_errors_take(hipStream_t s);
+// Test hooks: the next fused launch leaves message skip_msg's ready flag
+// unset (~0u: none); wait_us bounds the DEK wait (0: the 1 s default).
+void fused_debug(uint32_t skip_msg, uint64_t wait_us);
+// Timeouts seen by fused_errors_take so far (process-wide).
+uint64_t fused_timeouts();
 
 // The second half of launch_post alone: ChaCha20 keyed by the DEK already in
 // bytes [32,64) of each ref slot, ctext store, CID into bytes [0,32).

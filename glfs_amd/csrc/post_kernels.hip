@@ -951,8 +951,8 @@ __device__ __forceinline__ void tree_reduce(uint32_t *lds, uint32_t k,
 // subtree done, end, HW_ID, XCC_ID, 0, 0]; DEK pass at [0, 4096), CID pass
 // at [4096, 8192).  s_memrealtime: 100 MHz.
 __device__ uint64_t g_wgtime[8192][8];
-__device__ __forceinline__ void wgt(bool chacha, int slot) {
-  const uint32_t b = blockIdx.x + (chacha ? 4096u : 0u);
+__device__ __forceinline__ void wgt(bool chacha, uint32_t bid, int slot) {
+  const uint32_t b = bid + (chacha ? 4096u : 0u);  // the pass's own workgroup number
   if (threadIdx.x == 0 && b < 8192) {
     g_wgtime[b][slot] = __builtin_amdgcn_s_memrealtime();
     if (slot == 0) {
@@ -961,9 +961,9 @@ __device__ __forceinline__ void wgt(bool chacha, int slot) {
     }
   }
 }
-#define WGT(slot) wgt(CHACHA, slot)
+#define WGT(bid, slot) wgt(CHACHA, bid, slot)
 #else
-#define WGT(slot) (void)0
+#define WGT(bid, slot) (void)0
 #endif
 
 // A: ARX in the asm form (many waves per SIMD); false: the compiler's form,
@@ -973,14 +973,37 @@ __device__ __forceinline__ void wgt(bool chacha, int slot) {
 template <bool CHACHA>
 constexpr int kStageOf = (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
 
-// DEK ready flags of a fused split launch (k_pass_dc): the DEK pass stores
-// message j's DEK with agent-scope atomic stores, waits for them, then sets
-// ready[j] = epoch; the CID workgroups of message j wait for that.
+// State of a fused split launch (k_pass_dc), one per (device, stream):
+//  - ready[j] = epoch once message j's DEK is published (flags are never
+//    reset: each launch has a new epoch, zero is never one);
+//  - ticket: a counter that only grows; the workgroup that takes value
+//    tbase + k runs work item k (k < nd: DEK, else CID);
+//  - err: a word in pinned host memory, set when a CID workgroup gave up
+//    waiting for a DEK (the launch's results are then invalid and the host
+//    fails or repeats the post);
+//  - wait_ticks: that wait's bound in s_memrealtime ticks (100 MHz);
+//  - skip_msg: test hook -- the DEK of this message is written but its
+//    ready flag is not (~0u: none).
+struct DcState {
+  uint32_t nd;
+  uint32_t *ready;
+  uint32_t epoch;
+  uint32_t *ticket;
+  uint32_t tbase;
+  uint32_t *err;
+  uint64_t wait_ticks;
+  uint32_t skip_msg;
+};
+
+// The DEK pass stores message j's DEK with agent-scope atomic stores, waits
+// for them, then sets ready[j] = epoch; the CID workgroups of message j wait
+// for that.
 __device__ __forceinline__ void publish_dek(uint8_t *dst, const uint32_t (&w)[8],
-                                            uint32_t *ready, uint32_t epoch) {
+                                            const DcState &d, uint64_t j) {
   publish_cv(reinterpret_cast<uint32_t *>(dst), w);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(ready, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (j != d.skip_msg)
+    __hip_atomic_store(d.ready + j, d.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The body of one workgroup (number bid) of a pass.  FUSE: 0 = a pass of its
@@ -988,10 +1011,10 @@ __device__ __forceinline__ void publish_dek(uint8_t *dst, const uint32_t (&w)[8]
 // flag); 2 = the CID part (waits for its message's DEK).
 template <int G, bool CHACHA, bool ALIGNED, int A, int FUSE>
 __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *lds_u4,
-                                          uint32_t *ready, uint32_t epoch) {
+                                          const DcState *dc) {
   constexpr int kStageU4 = kStageOf<CHACHA>;
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
-  WGT(0);
+  WGT(bid, 0);
   // message j, sub-range sidx (split mode) = chunks [sidx*256G, +256G)
   const uint64_t j = bid >> a.split_log2;
   const uint32_t sidx = bid & ((1u << a.split_log2) - 1u);
@@ -1012,16 +1035,28 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   for (int i = 0; i < 8; ++i) key[i] = a.key[i];
   uint32_t dek[8];
   if constexpr (FUSE == 2) {
-    // this message's DEK, from the DEK workgroups of the same launch: they
-    // were all dispatched before any CID workgroup, so they complete; the
-    // wait is bounded anyway (200 ms of s_memrealtime at 100 MHz)
+    // this message's DEK, from the DEK work items of the same launch.  Work
+    // items are taken by ticket (k_pass_dc), so every DEK item was taken by
+    // a workgroup that was already running before this one took its CID
+    // item: the wait depends only on running workgroups, whatever the
+    // dispatch order or other launches sharing the chip.  It is bounded
+    // anyway; a timeout marks the launch failed in d.err (the host then
+    // discards its results) and the workgroup finishes with whatever key it
+    // read, so counters and flags stay consistent for later launches.
     if (t == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-             epoch) {
+      while (__hip_atomic_load(dc->ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+             dc->epoch) {
         __builtin_amdgcn_s_sleep(4);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > dc->wait_ticks) {
+          __hip_atomic_store(dc->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
+      // the DEK loads below must not be hoisted above the flag load that
+      // saw the epoch (a compiler barrier; the loads are agent-scope, so no
+      // cache invalidate is needed)
+      __atomic_signal_fence(__ATOMIC_ACQUIRE);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         lds[i] = load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i);
@@ -1073,7 +1108,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   }
   if (whole) {  // uniform: depends on len only; lane 0 holds the root output
     if (t == 0) {
-      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, *dc, j);
       else store_digest(ref + a.out_off, cv);
     }
     return;
@@ -1084,12 +1119,12 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
     for (int i = 0; i < 8; ++i) lds[t * 8 + i] = cv[i];
   }
   __syncthreads();
-  WGT(1);
+  WGT(bid, 1);
   tree_reduce(lds, active, t, key, a.base, !split, cv);
-  WGT(2);
+  WGT(bid, 2);
   if (!split) {
     if (t == 0) {
-      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+      if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, *dc, j);
       else store_digest(ref + a.out_off, cv);
     }
     return;
@@ -1111,7 +1146,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
     flag = &s_flag;
   }
   if (!arrive_last(a.cnt + j, W, t, flag)) {
-    WGT(3);
+    WGT(bid, 3);
     return;
   }
   if (t < W) {
@@ -1124,33 +1159,47 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   __syncthreads();
   tree_reduce(lds, W, t, key, a.base, true, cv);
   if (t == 0) {
-    if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, ready + j, epoch);
+    if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, *dc, j);
     else store_digest(ref + a.out_off, cv);
     a.cnt[j] = 0;
   }
-  WGT(3);
+  WGT(bid, 3);
 }
 
 template <int G, bool CHACHA, bool ALIGNED, int A = 2>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   __shared__ uint4 lds_u4[512 + kStageOf<CHACHA>];
-  pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr, 0u);
+  pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr);
 }
 
-// Both passes of a split-mode post in one launch: workgroups [0, nd) run the
-// DEK pass (a), the rest the ChaCha20+CID pass (b), each CID workgroup
-// starting as soon as its message's DEK is published.  Workgroups are
-// dispatched in index order, so every DEK workgroup is resident or done
-// before the first CID workgroup waits; the CID pass fills the DEK pass's
-// tail instead of waiting for the whole launch to drain.
+// Both passes of a split-mode post in one launch: work items [0, nd) run the
+// DEK pass (a), the rest the ChaCha20+CID pass (b), each CID item starting as
+// soon as its message's DEK is published, so the CID pass fills the DEK
+// pass's tail instead of waiting for the whole launch to drain.  A workgroup
+// takes its item by ticket (one device-wide atomic) rather than by
+// blockIdx: a CID item then only ever waits for DEK items that running
+// workgroups already hold, which needs no assumption about the order in
+// which the hardware dispatches workgroups, nor about other launches (other
+// streams, other processes) occupying the CUs.
 template <int G>
-__global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, uint32_t nd,
-                                                 uint32_t *ready, uint32_t epoch) {
+__global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
   __shared__ uint4 lds_u4[512 + kStageOf<true>];
-  if (blockIdx.x < nd)
-    pass_body<G, false, true, 2, 1>(a, blockIdx.x, lds_u4, ready, epoch);
+  uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
+  if (threadIdx.x == 0)
+    lds[0] = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) - d.tbase;
+  __syncthreads();
+  const uint32_t item = __builtin_amdgcn_readfirstlane(lds[0]);
+  __syncthreads();
+  if (item >= gridDim.x) {  // the host's ticket count is off: fail loudly
+    if (threadIdx.x == 0)
+      __hip_atomic_store(d.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  if (item < d.nd)
+    pass_body<G, false, true, 2, 1>(a, item, lds_u4, &d);
   else
-    pass_body<G, true, true, 2, 2>(b, blockIdx.x - nd, lds_u4, ready, epoch);
+    pass_body<G, true, true, 2, 2>(b, item - d.nd, lds_u4, &d);
 }
 
 // ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
@@ -2015,6 +2064,10 @@ struct ScratchSlot {
   uint32_t *ready;     // k_pass_dc: per-message DEK ready flags (= epoch)
   size_t ready_words;
   uint32_t epoch;
+  uint32_t *ticket;    // k_pass_dc: work-item counter (device memory)
+  uint32_t tickets;    // its value once every launch so far has run
+  uint32_t *err;       // k_pass_dc: DEK-wait timeouts (pinned host word)
+  uint32_t *d_err;     // the same word as the kernels address it
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
@@ -2029,7 +2082,8 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) {
-    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0});
+    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0, nullptr, 0,
+                         nullptr, nullptr});
     sl = &g_scratch.back();
   }
   if (sl->bytes < bytes || sl->cnt_words < words) {
@@ -2064,10 +2118,15 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   return hipSuccess;
 }
 
-// k_pass_dc's ready flags for msgs messages on stream s, and this launch's
-// epoch (flags hold the epoch of the launch that set them, so they are never
-// reset; zero is never an epoch).
-hipError_t ready_get(uint64_t msgs, hipStream_t s, uint32_t **ready, uint32_t *epoch) {
+// k_pass_dc's state for a launch of `wgs` workgroups over msgs messages on
+// stream s: the ready flags and this launch's epoch (flags hold the epoch of
+// the launch that set them, so they are never reset; zero is never an
+// epoch), the ticket counter and this launch's first ticket, the error word.
+std::atomic<uint64_t> g_dc_wait_ticks{100000000ull};  // 1 s of s_memrealtime
+std::atomic<uint32_t> g_dc_skip_msg{~0u};
+std::atomic<uint64_t> g_dc_timeouts{0};
+
+hipError_t dc_get(uint64_t msgs, uint64_t wgs, hipStream_t s, DcState *d) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -2076,6 +2135,24 @@ hipError_t ready_get(uint64_t msgs, hipStream_t s, uint32_t **ready, uint32_t *e
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) return hipErrorInvalidValue;  // scratch_get first
+  if (!sl->ticket) {
+    e = hipMalloc(reinterpret_cast<void **>(&sl->ticket), 4);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(sl->ticket, 0, 4, s);
+    if (e != hipSuccess) return e;
+    sl->tickets = 0;
+    void *h = nullptr, *dp = nullptr;
+    e = hipHostMalloc(&h, 64, hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    e = hipHostGetDevicePointer(&dp, h, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(h);
+      return e;
+    }
+    sl->err = static_cast<uint32_t *>(h);
+    sl->d_err = static_cast<uint32_t *>(dp);
+    __atomic_store_n(sl->err, 0u, __ATOMIC_RELAXED);
+  }
   if (sl->ready_words < msgs) {
     if (sl->ready) {
       e = hipStreamSynchronize(s);
@@ -2093,8 +2170,14 @@ hipError_t ready_get(uint64_t msgs, hipStream_t s, uint32_t **ready, uint32_t *e
     sl->epoch = 0;
   }
   if (++sl->epoch == 0) ++sl->epoch;
-  *ready = sl->ready;
-  *epoch = sl->epoch;
+  d->ready = sl->ready;
+  d->epoch = sl->epoch;
+  d->ticket = sl->ticket;
+  d->tbase = sl->tickets;  // launches on s run in order: all earlier ones
+  sl->tickets += uint32_t(wgs);  // have taken their tickets (mod 2^32)
+  d->err = sl->d_err;
+  d->wait_ticks = g_dc_wait_ticks.load(std::memory_order_relaxed);
+  d->skip_msg = g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed);
   return hipSuccess;
 }
 
@@ -2275,6 +2358,9 @@ void release_stream_scratch(hipStream_t s) {
     if (hipGetDevice(&cur) == hipSuccess && cur == g_scratch[i].dev) {
       if (g_scratch[i].p) (void)hipFree(g_scratch[i].p);
       if (g_scratch[i].cnt) (void)hipFree(g_scratch[i].cnt);
+      if (g_scratch[i].ready) (void)hipFree(g_scratch[i].ready);
+      if (g_scratch[i].ticket) (void)hipFree(g_scratch[i].ticket);
+      if (g_scratch[i].err) (void)hipHostFree(g_scratch[i].err);
     } else {
       continue;  // another device's stream of the same handle value
     }
@@ -2283,6 +2369,26 @@ void release_stream_scratch(hipStream_t s) {
     --i;
   }
 }
+
+uint32_t fused_errors_take(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (ScratchSlot &x : g_scratch)
+    if (x.dev == dev && x.stream == s && x.err) {
+      const uint32_t v = __atomic_exchange_n(x.err, 0u, __ATOMIC_ACQ_REL);
+      if (v) g_dc_timeouts.fetch_add(1, std::memory_order_relaxed);
+      return v;
+    }
+  return 0;
+}
+
+void fused_debug(uint32_t skip_msg, uint64_t wait_us) {
+  g_dc_skip_msg.store(skip_msg, std::memory_order_relaxed);
+  g_dc_wait_ticks.store(wait_us ? wait_us * 100 : 100000000ull, std::memory_order_relaxed);
+}
+
+uint64_t fused_timeouts() { return g_dc_timeouts.load(std::memory_order_relaxed); }
 
 void blake3_iv_words(uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) w[i] = kIV[i];
@@ -2336,9 +2442,9 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   a.split_log2 = sl;
   hipError_t e = scratch_get(&a, 2 * wgs, 2 * job.n, s);
   if (e != hipSuccess) return e;
-  uint32_t *ready;
-  uint32_t epoch;
-  e = ready_get(job.n, s, &ready, &epoch);
+  DcState d{};
+  d.nd = uint32_t(wgs);
+  e = dc_get(job.n, 2 * wgs, s, &d);
   if (e != hipSuccess) return e;
   KArgs b = a;
   for (int i = 0; i < 8; ++i) b.key[i] = job.cid_key[i];
@@ -2348,18 +2454,18 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   b.cnt = a.cnt + job.n;
   const dim3 grid(uint32_t(2 * wgs)), block(256);
   switch (g) {
-    case 1: hipLaunchKernelGGL(k_pass_dc<1>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
-    case 2: hipLaunchKernelGGL(k_pass_dc<2>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
-    default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, uint32_t(wgs), ready, epoch); break;
+    case 1: hipLaunchKernelGGL(k_pass_dc<1>, grid, block, 0, s, a, b, d); break;
+    case 2: hipLaunchKernelGGL(k_pass_dc<2>, grid, block, 0, s, a, b, d); break;
+    default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, d); break;
   }
   *done = true;
   return hipGetLastError();
 }
 
-hipError_t launch_post(const PostJob &job, hipStream_t s) {
+hipError_t launch_post(const PostJob &job, hipStream_t s, bool fused) {
   if (job.n == 0) return hipSuccess;
   bool done = false;
-  hipError_t e = launch_post_fused(job, s, &done);
+  hipError_t e = fused ? launch_post_fused(job, s, &done) : hipSuccess;
   if (e != hipSuccess || done) return e;
   e = launch_keyed_hash(job, 32, s);
   if (e != hipSuccess) return e;

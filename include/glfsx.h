@@ -106,6 +106,16 @@ uint32_t glfsx_set_split_target(uint32_t wgs);
  * are identical either way.  Returns the previous value; process-wide. */
 uint32_t glfsx_set_latency_wgs(uint32_t wgs);
 
+/* Test hooks (no reference counterpart).  A split-mode post of many
+ * workgroups runs both passes in one launch, each CID work item waiting for
+ * its block's DEK; a wait that exceeds its bound fails the launch loudly:
+ * the calls that synchronise repeat the post with two launches (Create,
+ * post_batch, the Writer) and count it.  glfsx_debug_fused makes the next
+ * such launch leave block skip_msg's DEK unpublished (~0u: none) and sets
+ * the bound to wait_us microseconds (0: the default, 1 s).  Returns the
+ * number of failed one-launch posts seen so far, process-wide. */
+uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);
+
 /* --- primitives -------------------------------------------------------- */
 /* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input, first out_len
  * (<= 32) bytes of the XOF. */
@@ -179,6 +189,15 @@ int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
 /* Deliver the Posts of every complete block written so far (no reference
  * counterpart: the reference never holds a complete block back). */
 int glfsx_writer_flush(glfsx_writer *w);
+/* Hash this writer's batches on several GPUs (no reference counterpart:
+ * one bigblob.Writer fed from one io.Reader): batch k of
+ * complete blocks runs on devs[k % ndev], each device with its own streams
+ * and pinned staging (one PCIe link each); Posts and the index build still
+ * replay in block order (blob.go:152-206), so the Post log and root are
+ * those of the one-device writer.  Call before the first write.  Index
+ * nodes and the tail block stay on the writer's own device; the device-input
+ * calls (write_device / write_ctext) need a one-device writer. */
+int glfsx_writer_set_devices(glfsx_writer *w, const int *devs, int ndev);
 /* strict != 0: blob.go:120-133 error timing (see glfsx_writer_write). */
 int glfsx_writer_set_strict(glfsx_writer *w, int strict);
 /* Text of the last failed call on this writer (any thread). */
@@ -200,6 +219,25 @@ int glfsx_create_device(uint64_t block_size, const uint8_t *salt,
                         const uint8_t *cid_key, const void *d_data,
                         uint64_t size, void *d_ctext, glfsx_root *out,
                         uint64_t *n_posts, void *stream);
+
+/* Create over a blob whose bytes lie on several devices, in one process
+ * (SURVEY 8e): the blob is the concatenation of nparts parts, part k of
+ * part_sizes[k] bytes at device pointer d_parts[k] on device devs[k] (a
+ * device may appear more than once).  Every part but the last must hold
+ * whole level-1 nodes (a positive multiple of block_size * block_size/64
+ * bytes: 16 GiB at 1 MiB blocks); the last is non-empty.  Each part's data
+ * blocks and level-1 index nodes are posted on its device, all parts at
+ * once (one host worker thread per part); the level-1 refs are gathered on
+ * the host and the levels above posted on devs[0].  d_ctexts (nullable, or
+ * entries NULL): ctext of part k, same layout as d_parts[k].  level1_out
+ * (nullable): with nparts > 1, the ceil(n0/bf) level-1 refs (64 B each).
+ * Calls are serialised.  Same root as glfsx_create_device over the whole
+ * blob. */
+int glfsx_create_devices(uint64_t block_size, const uint8_t *salt,
+                         const uint8_t *cid_key, int nparts, const int *devs,
+                         const void *const *d_parts, const uint64_t *part_sizes,
+                         void *const *d_ctexts, uint8_t *level1_out,
+                         glfsx_root *out, uint64_t *n_posts);
 
 /* Multi-GPU shard: posts blocks [first_block, first_block + nb)
  * of a blob of `size` bytes whose bytes for that range are at d_range, plus
