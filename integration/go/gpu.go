@@ -1,0 +1,253 @@
+//go:build glfsgpu
+
+// The bigblob write path on MI355X: with -tags glfsgpu, every
+// bigblob.Writer (and so glfs.PostBlob / PostTyped / TypedWriter / PostTree
+// and bigblob.Create / Concat) hashes through libglfsx (include/glfsx.h).
+// Goes to bigblob/gpu.go of blobcache/glfs; bigblob_gpu.patch adds the
+// delegation to blob.go.  Build: CGO_CFLAGS=-I<glfsx>/include
+// CGO_LDFLAGS="-L<glfsx>/lib -lglfsx" go build -tags glfsgpu ./...
+//
+// Environment:
+//   GLFSX_STRICT=1   blob.go:120-133 error timing (a store error comes back
+//                    from the Write that completed the failing block); the
+//                    default 0 pipelines 64 MiB batches and returns it from
+//                    the Write or Finish whose batch held it -- the Posts
+//                    are the same prefix either way, and Create returns the
+//                    same error.
+//   GLFSX_DEVICES=0,1,...  hash each Writer's batches round-robin on these
+//                    GPUs (one Writer fed by one io.Reader over several PCIe
+//                    links; Posts still in block order).
+//   GLFSX_PARITY=k   re-hash every k-th Post through the store's own Post
+//                    and compare CIDs (parity mode).
+
+package bigblob
+
+/*
+#cgo LDFLAGS: -lglfsx
+#include <stdlib.h>
+#include <string.h>
+#include "glfsx.h"
+
+// C cannot call a Go func value: the writer's cgo.Handle travels through
+// post_ctx and goPost dispatches on it.
+extern int goPost(void *ctx, int kind, uint8_t *ref, void *ctext, uint64_t len);
+static int post_tramp(void *ctx, int kind, const uint8_t *ref, const void *ctext,
+                      uint64_t len) {
+	return goPost(ctx, kind, (uint8_t *)ref, (void *)ctext, len);
+}
+
+// glfsx_last_error() is thread-local and a goroutine may move to another OS
+// thread between two cgo calls, so each wrapper copies the error text in the
+// SAME C call that failed.
+static void copy_err(char *err, size_t cap) {
+	strncpy(err, glfsx_last_error(), cap - 1);
+	err[cap - 1] = 0;
+}
+static glfsx_writer *writer_new(uint64_t bs, uint64_t max, const uint8_t *salt,
+                                void *h, int *rc, char *err, size_t cap) {
+	glfsx_writer *w = glfsx_writer_new(bs, max, salt, NULL, post_tramp, h, rc);
+	if (!w) copy_err(err, cap);
+	return w;
+}
+static int writer_devices(glfsx_writer *w, const int *devs, int n, char *err, size_t cap) {
+	int rc = glfsx_writer_set_devices(w, devs, n);
+	if (rc) copy_err(err, cap);
+	return rc;
+}
+static int derive_key(uint8_t *out, size_t n, const uint8_t *salt, const void *in,
+                      size_t len, char *err, size_t cap) {
+	int rc = glfsx_derive_key(out, n, salt, in, len);
+	if (rc) copy_err(err, cap);
+	return rc;
+}
+*/
+import "C"
+
+import (
+	"context"
+	"errors"
+	"fmt"
+	"os"
+	"runtime/cgo"
+	"strconv"
+	"strings"
+	"unsafe"
+
+	"blobcache.io/blobcache/src/bcsdk"
+	"blobcache.io/blobcache/src/blobcache"
+)
+
+// PrehashedWO is implemented by stores that accept a CID the caller computed
+// (the GPU already hashed every ctext): no second BLAKE3 pass on the host.
+// glfsx_store (include/glfsx.h) is such a store; a blobcache client would add
+// PostHashed next to Post.
+type PrehashedWO interface {
+	PostHashed(ctx context.Context, cid blobcache.CID, data []byte) error
+}
+
+var (
+	parityEvery = envInt("GLFSX_PARITY", 0)
+	strict      = envInt("GLFSX_STRICT", 0)
+	devices     = envInts("GLFSX_DEVICES")
+)
+
+type gpuWriter struct {
+	w   *C.glfsx_writer
+	s   bcsdk.WO
+	ctx context.Context
+	err error // the store's error, returned by the Write/Finish that saw it
+	h   cgo.Handle
+	n   uint64
+}
+
+// newGPUWriter mirrors blob.go:85-114 (NewWriter): block size 0 means the
+// store's MaxSize (bigblob machine.go:22-30), a nil salt is 0^32.
+func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte) *Writer {
+	if C.glfsx_device_count() == 0 {
+		return nil // no GPU: the Go path (the library has no CPU fallback)
+	}
+	gw := &gpuWriter{s: s, ctx: context.TODO()}
+	gw.h = cgo.NewHandle(gw)
+	var csalt *C.uint8_t
+	if salt != nil {
+		csalt = (*C.uint8_t)(unsafe.Pointer(&salt[0])) // read during the call only
+	}
+	var rc C.int
+	var cerr [512]C.char
+	gw.w = C.writer_new(C.uint64_t(ag.blockSize), C.uint64_t(s.MaxSize()), csalt,
+		unsafe.Pointer(uintptr(gw.h)), &rc, &cerr[0], C.size_t(len(cerr)))
+	if gw.w == nil {
+		gw.h.Delete()
+		msg := C.GoString(&cerr[0])
+		switch rc {
+		case C.GLFSX_E_BLOCKSIZE_GT_MAX, C.GLFSX_E_BLOCKSIZE_LT_MIN:
+			panic(msg) // blob.go:91 "blockSize %d > maxSize %d", :94 "blockSize cannot be < 128"
+		default:
+			panic(fmt.Errorf("glfsx %d: %s", int(rc), msg))
+		}
+	}
+	C.glfsx_writer_set_strict(gw.w, C.int(strict))
+	if len(devices) > 0 {
+		cdevs := (*C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))
+		defer C.free(unsafe.Pointer(cdevs))
+		ds := unsafe.Slice(cdevs, len(devices))
+		for i, d := range devices {
+			ds[i] = C.int(d)
+		}
+		if rc := C.writer_devices(gw.w, cdevs, C.int(len(devices)), &cerr[0],
+			C.size_t(len(cerr))); rc != 0 {
+			gw.close()
+			panic(fmt.Errorf("glfsx %d: %s", int(rc), C.GoString(&cerr[0])))
+		}
+	}
+	return &Writer{gpu: gw}
+}
+
+//export goPost
+func goPost(ctx unsafe.Pointer, kind C.int, ref *C.uint8_t, ctext unsafe.Pointer, n C.uint64_t) C.int {
+	gw := cgo.Handle(uintptr(ctx)).Value().(*gpuWriter)
+	// ctext is C memory, valid only during this call; the store copies it
+	var data []byte
+	if n > 0 {
+		data = unsafe.Slice((*byte)(ctext), int(n))
+	}
+	var cid blobcache.CID
+	copy(cid[:], unsafe.Slice((*byte)(unsafe.Pointer(ref)), 32))
+	gw.n++
+	if ps, ok := gw.s.(PrehashedWO); ok && (parityEvery == 0 || gw.n%uint64(parityEvery) != 0) {
+		if err := ps.PostHashed(gw.ctx, cid, data); err != nil { // no host BLAKE3
+			gw.err = err
+			return 1
+		}
+		return 0
+	}
+	got, err := gw.s.Post(gw.ctx, data) // ref.go:103: the store hashes
+	if err != nil {
+		gw.err = err
+		return 1
+	}
+	if got != cid { // parity: the store's CID must equal the GPU's
+		gw.err = fmt.Errorf("glfsx: store CID %v != GPU CID %v", got, cid)
+		return 2
+	}
+	return 0
+}
+
+func (gw *gpuWriter) fail(rc C.int) error {
+	if rc == C.GLFSX_E_STORE && gw.err != nil {
+		return gw.err
+	}
+	// the writer keeps its own error text: safe from any OS thread
+	return fmt.Errorf("glfsx %d: %s", int(rc), C.GoString(C.glfsx_writer_error(gw.w)))
+}
+
+// Write mirrors blob.go:120-133.  Go memory is passed for the duration of the
+// call only (cgo pointer rules); the C side copies it into pinned staging.
+func (gw *gpuWriter) Write(data []byte) (int, error) {
+	if len(data) == 0 {
+		return 0, nil
+	}
+	if rc := C.glfsx_writer_write(gw.w, unsafe.Pointer(&data[0]), C.size_t(len(data))); rc != 0 {
+		return 0, gw.fail(rc)
+	}
+	return len(data), nil
+}
+
+// Finish mirrors blob.go:135-150.
+func (gw *gpuWriter) Finish(ctx context.Context) (*Root, error) {
+	gw.ctx = ctx
+	defer gw.close()
+	var r C.glfsx_root
+	if rc := C.glfsx_writer_finish(gw.w, &r); rc != 0 {
+		return nil, gw.fail(rc)
+	}
+	ref, err := RefFromBytes(C.GoBytes(unsafe.Pointer(&r.ref[0]), 64))
+	if err != nil {
+		return nil, err
+	}
+	return &Root{Ref: *ref, Size: uint64(r.size), BlockSize: uint64(r.block_size)}, nil
+}
+
+func (gw *gpuWriter) close() {
+	if gw.w != nil {
+		C.glfsx_writer_free(gw.w)
+		gw.w = nil
+		gw.h.Delete()
+	}
+}
+
+// DeriveKeyGPU is DeriveKey (ref.go:152-161) on the GPU: any len(out), any
+// input length.
+func DeriveKeyGPU(out []byte, salt *[32]byte, input []byte) {
+	if len(out) == 0 {
+		return
+	}
+	var in unsafe.Pointer
+	if len(input) > 0 {
+		in = unsafe.Pointer(&input[0])
+	}
+	var cerr [512]C.char
+	if rc := C.derive_key((*C.uint8_t)(unsafe.Pointer(&out[0])), C.size_t(len(out)),
+		(*C.uint8_t)(unsafe.Pointer(&salt[0])), in, C.size_t(len(input)),
+		&cerr[0], C.size_t(len(cerr))); rc != 0 {
+		panic(errors.New(C.GoString(&cerr[0]))) // DeriveKey panics too (ref.go:155,159)
+	}
+}
+
+func envInt(k string, def int) int {
+	v, err := strconv.Atoi(os.Getenv(k))
+	if err != nil {
+		return def
+	}
+	return v
+}
+
+func envInts(k string) []int {
+	var out []int
+	for _, f := range strings.Split(os.Getenv(k), ",") {
+		if v, err := strconv.Atoi(strings.TrimSpace(f)); err == nil {
+			out = append(out, v)
+		}
+	}
+	return out
+}

@@ -1,0 +1,20 @@
+//go:build !glfsgpu
+
+// Without the glfsgpu build tag the bigblob write path is the reference's
+// own Go code: newGPUWriter returns nil and blob.go's Writer runs unchanged.
+// Goes to bigblob/gpu_stub.go of blobcache/glfs (see bigblob_gpu.patch).
+
+package bigblob
+
+import (
+	"context"
+
+	"blobcache.io/blobcache/src/bcsdk"
+)
+
+type gpuWriter struct{ ctx context.Context }
+
+func (gw *gpuWriter) Write([]byte) (int, error)             { panic("unreachable") }
+func (gw *gpuWriter) Finish(context.Context) (*Root, error) { panic("unreachable") }
+
+func (ag *Machine) newGPUWriter(bcsdk.WO, *[32]byte) *Writer { return nil }

@@ -1,0 +1,108 @@
+"""The reference-side binding (integration/go/) is real: the patch applies to
+the reference's bigblob/blob.go, the cgo preamble compiles against
+include/glfsx.h, and every C symbol and Go hook it uses exists.
+
+There is no Go toolchain in this image, so the Go files are
+checked structurally; the C half of the cgo binding is compiled with gcc.
+`git apply --check` only reads /root/reference (nothing is written there).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GO = os.path.join(ROOT, "integration", "go")
+REF = "/root/reference"
+
+
+def _read(name):
+    with open(os.path.join(GO, name)) as f:
+        return f.read()
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "bigblob")) or not shutil.which("git"),
+                    reason="the reference checkout is only in the build container")
+def test_patch_applies_to_reference():
+    p = subprocess.run(["git", "apply", "--check", "-v", os.path.join(GO, "bigblob_gpu.patch")],
+                       cwd=REF, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    assert "Checking patch bigblob/blob.go" in p.stderr
+
+
+def test_patch_hooks_exist_in_both_builds():
+    """What the patched blob.go calls (newGPUWriter, gpu.ctx, gpu.Write,
+    gpu.Finish, the gpu field's type) is defined with and without the
+    glfsgpu tag, with the reference's types (bcsdk.WO, blob.go:85)."""
+    patch = _read("bigblob_gpu.patch")
+    added = "\n".join(ln[1:] for ln in patch.splitlines()
+                      if ln.startswith("+") and not ln.startswith("+++"))
+    assert "ag.newGPUWriter(s, salt)" in added
+    assert "w.gpu.Write(data)" in added and "w.gpu.Finish(ctx)" in added
+    assert "w.gpu.ctx = ctx" in added and "gpu *gpuWriter" in added
+    # context lines are the reference's own (blob.go:85-86)
+    assert " func (ag *Machine) NewWriter(s bcsdk.WO, salt *[32]byte) *Writer {" in patch
+    assert " \tblockSize := s.MaxSize()" in patch
+    for name, tag in (("gpu.go", "//go:build glfsgpu"), ("gpu_stub.go", "//go:build !glfsgpu")):
+        src = _read(name)
+        assert src.startswith(tag + "\n"), name
+        assert re.search(r"^package bigblob$", src, re.M), name
+        assert re.search(r"type gpuWriter struct\s*\{[^}]*\bctx\s+context\.Context", src, re.S), name
+        assert re.search(r"func \(ag \*Machine\) newGPUWriter\((s )?bcsdk\.WO, (salt )?\*\[32\]byte\) "
+                         r"\*Writer", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) Write\((data )?\[\]byte\) \(int, error\)", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) Finish\((ctx )?context\.Context\) "
+                         r"\(\*Root, error\)", src), name
+        assert "schema.WO" not in src, name
+        assert src.count("{") == src.count("}"), name
+        assert src.count("(") == src.count(")"), name
+
+
+def test_cgo_symbols_are_in_the_header():
+    hdr = open(os.path.join(ROOT, "include", "glfsx.h")).read()
+    src = _read("gpu.go")
+    used = set(re.findall(r"\b(glfsx_\w+)", src))
+    assert used, "no C symbols?"
+    for sym in sorted(used):
+        assert re.search(r"\b" + sym + r"\b", hdr), sym
+    for const in set(re.findall(r"C\.(GLFSX_\w+)", src)):
+        assert re.search(r"\b" + const + r"\b", hdr), const
+
+
+@pytest.mark.skipif(not shutil.which("gcc"), reason="no gcc")
+def test_cgo_preamble_compiles(tmp_path):
+    """The cgo preamble of gpu.go is plain C over glfsx.h: compile it with
+    gcc -Werror (goPost, which cgo generates from the //export, is stubbed)."""
+    src = _read("gpu.go")
+    m = re.search(r"/\*\n(.*?)\*/\nimport \"C\"", src, re.S)
+    assert m, "no cgo preamble"
+    pre = "\n".join(ln for ln in m.group(1).splitlines() if not ln.startswith("#cgo"))
+    c = tmp_path / "preamble.c"
+    c.write_text(pre + """
+int goPost(void *ctx, int kind, uint8_t *ref, void *ctext, uint64_t len) {
+  (void)ctx; (void)kind; (void)ref; (void)ctext; (void)len; return 0;
+}
+void *touch(void) {
+  static void *fns[4];
+  fns[0] = (void *)writer_new; fns[1] = (void *)writer_devices;
+  fns[2] = (void *)derive_key; fns[3] = (void *)post_tramp;
+  return fns;
+}
+""")
+    p = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-c",
+                        "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                        str(tmp_path / "preamble.o")], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
+def test_integration_md_embeds_the_shipped_files():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "embed_integration", os.path.join(ROOT, "scripts", "embed_integration.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert text.count("<!-- embed: integration/go/") == 3
+    assert mod.render(text) == text, "run scripts/embed_integration.py"
