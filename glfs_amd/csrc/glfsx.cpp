@@ -169,7 +169,7 @@ int fused_check(hipStream_t s) {
     return fail(GLFSX_E_DEVICE,
                 "one-launch split post on stream %p: %s; its results were discarded",
                 static_cast<void *>(s),
-                v == 1 ? "a DEK wait timed out" : "work-item tickets out of range");
+                v == 1 ? "a DEK wait timed out" : "a workgroup found no work item");
   }
   return 0;
 }

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -973,26 +974,39 @@ __device__ __forceinline__ void wgt(bool chacha, uint32_t bid, int slot) {
 template <bool CHACHA>
 constexpr int kStageOf = (CHACHA ? GLFSX_LDS_CTEXT : GLFSX_LDS_LOADS) ? 4 * 512 : 0;
 
-// State of a fused split launch (k_pass_dc), one per (device, stream):
+// State of a fused split launch (k_pass_dc).  Per (device, stream), in
+// device memory (DcConst), read where it is used -- as kernel arguments
+// these words would stay live in SGPRs through the whole body (the DEK/CID
+// bodies then spilled SGPRs: 4 -> 33 at G = 2):
 //  - ready[j] = epoch once message j's DEK is published (flags are never
 //    reset: each launch has a new epoch, zero is never one);
-//  - ticket: a counter that only grows; the workgroup that takes value
-//    tbase + k runs work item k (k < nd: DEK, else CID);
+//  - lists: two banks of kLists work-list counters, one per 128-B line
+//    (k_pass_dc); launch e uses bank e & 1 and zeroes bank (e + 1) & 1 for
+//    the next launch on the stream;
 //  - err: a word in pinned host memory, set when a CID workgroup gave up
-//    waiting for a DEK (the launch's results are then invalid and the host
-//    fails or repeats the post);
+//    waiting for a DEK, or found no work item (the launch's results are
+//    then invalid and the host fails or repeats the post);
 //  - wait_ticks: that wait's bound in s_memrealtime ticks (100 MHz);
 //  - skip_msg: test hook -- the DEK of this message is written but its
 //    ready flag is not (~0u: none).
-struct DcState {
-  uint32_t nd;
+constexpr uint32_t kLists = 8;           // one per XCD
+constexpr uint32_t kListStride = 32;     // words between counters (128 B)
+struct DcConst {
   uint32_t *ready;
-  uint32_t epoch;
-  uint32_t *ticket;
-  uint32_t tbase;
+  uint32_t *lists;
   uint32_t *err;
   uint64_t wait_ticks;
   uint32_t skip_msg;
+};
+// Per launch (kernel argument): the epoch, and the messages and log2
+// workgroups per message of both passes (a.n, a.split_log2, given again so
+// the item search does not touch the pass arguments: reading those before
+// the branch made the bodies spill SGPRs).
+struct DcState {
+  uint32_t epoch;
+  uint32_t n;
+  uint32_t sl;
+  const DcConst *c;
 };
 
 // The DEK pass stores message j's DEK with agent-scope atomic stores, waits
@@ -1002,8 +1016,9 @@ __device__ __forceinline__ void publish_dek(uint8_t *dst, const uint32_t (&w)[8]
                                             const DcState &d, uint64_t j) {
   publish_cv(reinterpret_cast<uint32_t *>(dst), w);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (j != d.skip_msg)
-    __hip_atomic_store(d.ready + j, d.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const DcConst *c = d.c;
+  if (j != c->skip_msg)
+    __hip_atomic_store(c->ready + j, d.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The body of one workgroup (number bid) of a pass.  FUSE: 0 = a pass of its
@@ -1036,7 +1051,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   uint32_t dek[8];
   if constexpr (FUSE == 2) {
     // this message's DEK, from the DEK work items of the same launch.  Work
-    // items are taken by ticket (k_pass_dc), so every DEK item was taken by
+    // items are taken from work lists (k_pass_dc), so every DEK item was taken by
     // a workgroup that was already running before this one took its CID
     // item: the wait depends only on running workgroups, whatever the
     // dispatch order or other launches sharing the chip.  It is bounded
@@ -1045,11 +1060,12 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
     // read, so counters and flags stay consistent for later launches.
     if (t == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(dc->ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+      const DcConst *c = dc->c;  // (the DEK items this one waits for precede it in its list)
+      while (__hip_atomic_load(c->ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
              dc->epoch) {
         __builtin_amdgcn_s_sleep(4);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > dc->wait_ticks) {
-          __hip_atomic_store(dc->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > c->wait_ticks) {
+          __hip_atomic_store(c->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -1172,34 +1188,72 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr);
 }
 
-// Both passes of a split-mode post in one launch: work items [0, nd) run the
-// DEK pass (a), the rest the ChaCha20+CID pass (b), each CID item starting as
-// soon as its message's DEK is published, so the CID pass fills the DEK
-// pass's tail instead of waiting for the whole launch to drain.  A workgroup
-// takes its item by ticket (one device-wide atomic) rather than by
-// blockIdx: a CID item then only ever waits for DEK items that running
-// workgroups already hold, which needs no assumption about the order in
-// which the hardware dispatches workgroups, nor about other launches (other
-// streams, other processes) occupying the CUs.
+// Both passes of a split-mode post in one launch: the DEK items run the DEK
+// pass (a), the CID items the ChaCha20+CID pass (b), each CID item starting
+// as soon as its message's DEK is published, so the CID pass fills the DEK
+// pass's tail instead of waiting for the whole launch to drain.
+//
+// Work is taken from kLists lists, not by blockIdx: list x holds the items
+// of messages j = x, x + 8, ... -- all their DEK items, then all their CID
+// items -- and hands them out in that order through one device-wide
+// counter.  A workgroup takes from the list of its own XCD first and moves
+// on to the others when that one is used up.  A CID item then only ever
+// waits for DEK items of its own list, which were handed out before it to
+// workgroups that were already running: the wait needs no assumption about
+// the order in which the hardware dispatches workgroups, how it places them
+// on XCDs, or other launches (streams, processes) occupying the CUs.  Every
+// workgroup finds an item (as many items as workgroups, each handed out
+// once).  One counter per XCD keeps the start of the launch from queueing
+// all 1024 first workgroups on one word (a single counter cost config 2
+// 1.7 %), and keeps a message's DEK and CID items on one XCD.
 template <int G>
 __global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
   __shared__ uint4 lds_u4[512 + kStageOf<true>];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
-  if (threadIdx.x == 0)
-    lds[0] = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) - d.tbase;
+  // thread 0 finds the item and leaves (workgroup number within its pass,
+  // kind: 0 DEK, 1 CID, 2 none) in LDS; only those two words stay live
+  if (threadIdx.x == 0) {
+    const uint32_t sl = d.sl;
+    const uint32_t n = d.n;
+    uint32_t *bank = d.c->lists + (d.epoch & 1u) * kLists * kListStride;
+    if (blockIdx.x == 0) {  // the next launch's counters (this stream's last
+      uint32_t *nb = d.c->lists + ((d.epoch + 1u) & 1u) * kLists * kListStride;
+      for (uint32_t x = 0; x < kLists; ++x)  // user of them has completed)
+        __hip_atomic_store(nb + x * kListStride, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & (kLists - 1u);
+    uint32_t bid = 0, kind = 2;
+    for (uint32_t k = 0; k < kLists; ++k) {
+      const uint32_t x = (xcc + k) & (kLists - 1u);
+      const uint32_t msgs = n > x ? (n - x + kLists - 1u) / kLists : 0u;
+      if (msgs == 0) continue;
+      const uint32_t t = __hip_atomic_fetch_add(bank + x * kListStride, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t nd = msgs << sl;
+      if (t < 2u * nd) {
+        const uint32_t u = t < nd ? t : t - nd;  // index within the list's pass
+        bid = ((x + kLists * (u >> sl)) << sl) | (u & ((1u << sl) - 1u));
+        kind = t < nd ? 0u : 1u;
+        break;
+      }
+    }
+    lds[0] = bid;
+    lds[1] = kind;
+  }
   __syncthreads();
-  const uint32_t item = __builtin_amdgcn_readfirstlane(lds[0]);
+  const uint32_t bid = __builtin_amdgcn_readfirstlane(lds[0]);
+  const uint32_t kind = __builtin_amdgcn_readfirstlane(lds[1]);
   __syncthreads();
-  if (item >= gridDim.x) {  // the host's ticket count is off: fail loudly
+  if (kind == 2) {  // no item left anywhere: counters were not at zero
     if (threadIdx.x == 0)
-      __hip_atomic_store(d.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d.c->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
-  if (item < d.nd)
-    pass_body<G, false, true, 2, 1>(a, item, lds_u4, &d);
+  if (kind == 0)
+    pass_body<G, false, true, 2, 1>(a, bid, lds_u4, &d);
   else
-    pass_body<G, true, true, 2, 2>(b, item - d.nd, lds_u4, &d);
+    pass_body<G, true, true, 2, 2>(b, bid, lds_u4, &d);
 }
 
 // ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
@@ -2064,10 +2118,11 @@ struct ScratchSlot {
   uint32_t *ready;     // k_pass_dc: per-message DEK ready flags (= epoch)
   size_t ready_words;
   uint32_t epoch;
-  uint32_t *ticket;    // k_pass_dc: work-item counter (device memory)
-  uint32_t tickets;    // its value once every launch so far has run
+  uint32_t *lists;     // k_pass_dc: 2 banks of work-list counters (device)
   uint32_t *err;       // k_pass_dc: DEK-wait timeouts (pinned host word)
   uint32_t *d_err;     // the same word as the kernels address it
+  DcConst *dcc;        // k_pass_dc's DcConst (device memory)
+  DcConst dcc_host;    // what was last copied there
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
@@ -2082,8 +2137,8 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) {
-    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0, nullptr, 0,
-                         nullptr, nullptr});
+    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0, nullptr,
+                         nullptr, nullptr, nullptr, DcConst{}});
     sl = &g_scratch.back();
   }
   if (sl->bytes < bytes || sl->cnt_words < words) {
@@ -2118,15 +2173,17 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   return hipSuccess;
 }
 
-// k_pass_dc's state for a launch of `wgs` workgroups over msgs messages on
-// stream s: the ready flags and this launch's epoch (flags hold the epoch of
-// the launch that set them, so they are never reset; zero is never an
-// epoch), the ticket counter and this launch's first ticket, the error word.
+// k_pass_dc's state for a launch over msgs messages on stream s: the ready
+// flags and this launch's epoch (flags hold the epoch of the launch that set
+// them, so they are never reset; zero is never an epoch), the work-list
+// counters (bank epoch & 1, at zero), the error word.
 std::atomic<uint64_t> g_dc_wait_ticks{100000000ull};  // 1 s of s_memrealtime
 std::atomic<uint32_t> g_dc_skip_msg{~0u};
 std::atomic<uint64_t> g_dc_timeouts{0};
 
-hipError_t dc_get(uint64_t msgs, uint64_t wgs, hipStream_t s, DcState *d) {
+constexpr size_t kListWords = 2 * kLists * kListStride;
+
+hipError_t dc_get(uint64_t msgs, hipStream_t s, DcState *d) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -2135,12 +2192,11 @@ hipError_t dc_get(uint64_t msgs, uint64_t wgs, hipStream_t s, DcState *d) {
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) return hipErrorInvalidValue;  // scratch_get first
-  if (!sl->ticket) {
-    e = hipMalloc(reinterpret_cast<void **>(&sl->ticket), 4);
+  if (!sl->lists) {
+    e = hipMalloc(reinterpret_cast<void **>(&sl->lists), kListWords * 4);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(sl->ticket, 0, 4, s);
+    e = hipMemsetAsync(sl->lists, 0, kListWords * 4, s);
     if (e != hipSuccess) return e;
-    sl->tickets = 0;
     void *h = nullptr, *dp = nullptr;
     e = hipHostMalloc(&h, 64, hipHostMallocCoherent);
     if (e != hipSuccess) return e;
@@ -2166,18 +2222,31 @@ hipError_t dc_get(uint64_t msgs, uint64_t wgs, hipStream_t s, DcState *d) {
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(sl->ready, 0, want * 4, s);
     if (e != hipSuccess) return e;
-    sl->ready_words = want;
-    sl->epoch = 0;
+    sl->ready_words = want;  // the epoch goes on: the new flags are zero
   }
-  if (++sl->epoch == 0) ++sl->epoch;
-  d->ready = sl->ready;
+  // zero is never an epoch; the bank parity must alternate across the wrap
+  if (++sl->epoch == 0) sl->epoch = 2;
+  DcConst want{sl->ready, sl->lists, sl->d_err,
+               g_dc_wait_ticks.load(std::memory_order_relaxed),
+               g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed)};
+  if (!sl->dcc) {
+    e = hipMalloc(reinterpret_cast<void **>(&sl->dcc), sizeof(DcConst));
+    if (e != hipSuccess) return e;
+    sl->dcc_host = DcConst{};
+  }
+  const DcConst &h = sl->dcc_host;
+  if (want.ready != h.ready || want.lists != h.lists || want.err != h.err ||
+      want.wait_ticks != h.wait_ticks || want.skip_msg != h.skip_msg) {
+    // rare (new buffers, a test hook): ordered on s before the launch; the
+    // copy is staged from pageable memory, so `want` may go out of scope
+    e = hipMemcpyAsync(sl->dcc, &want, sizeof want, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    sl->dcc_host = want;
+  }
   d->epoch = sl->epoch;
-  d->ticket = sl->ticket;
-  d->tbase = sl->tickets;  // launches on s run in order: all earlier ones
-  sl->tickets += uint32_t(wgs);  // have taken their tickets (mod 2^32)
-  d->err = sl->d_err;
-  d->wait_ticks = g_dc_wait_ticks.load(std::memory_order_relaxed);
-  d->skip_msg = g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed);
+  d->c = sl->dcc;
   return hipSuccess;
 }
 
@@ -2359,8 +2428,9 @@ void release_stream_scratch(hipStream_t s) {
       if (g_scratch[i].p) (void)hipFree(g_scratch[i].p);
       if (g_scratch[i].cnt) (void)hipFree(g_scratch[i].cnt);
       if (g_scratch[i].ready) (void)hipFree(g_scratch[i].ready);
-      if (g_scratch[i].ticket) (void)hipFree(g_scratch[i].ticket);
+      if (g_scratch[i].lists) (void)hipFree(g_scratch[i].lists);
       if (g_scratch[i].err) (void)hipHostFree(g_scratch[i].err);
+      if (g_scratch[i].dcc) (void)hipFree(g_scratch[i].dcc);
     } else {
       continue;  // another device's stream of the same handle value
     }
@@ -2377,7 +2447,12 @@ uint32_t fused_errors_take(hipStream_t s) {
   for (ScratchSlot &x : g_scratch)
     if (x.dev == dev && x.stream == s && x.err) {
       const uint32_t v = __atomic_exchange_n(x.err, 0u, __ATOMIC_ACQ_REL);
-      if (v) g_dc_timeouts.fetch_add(1, std::memory_order_relaxed);
+      if (v) {
+        g_dc_timeouts.fetch_add(1, std::memory_order_relaxed);
+        // a failed launch may leave its counters off zero (it zeroes the
+        // other bank); both banks start over at zero
+        (void)hipMemsetAsync(x.lists, 0, kListWords * 4, s);
+      }
       return v;
     }
   return 0;
@@ -2443,9 +2518,10 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   hipError_t e = scratch_get(&a, 2 * wgs, 2 * job.n, s);
   if (e != hipSuccess) return e;
   DcState d{};
-  d.nd = uint32_t(wgs);
-  e = dc_get(job.n, 2 * wgs, s, &d);
+  e = dc_get(job.n, s, &d);
   if (e != hipSuccess) return e;
+  d.n = uint32_t(job.n);
+  d.sl = sl;
   KArgs b = a;
   for (int i = 0; i < 8; ++i) b.key[i] = job.cid_key[i];
   b.base = job.cid_keyed ? kKeyed : 0u;
