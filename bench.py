@@ -189,11 +189,23 @@ def main():
             if "sinks" in hrt:   # aggregates too, like value
                 hrt["sinks"] = {k: round(world * v, 2) for k, v in hrt["sinks"].items()}
             hrt["what"] += f"; {world} ranks at once, aggregate over the slowest rank"
+        if world > 1:
+            # SURVEY 8e in ONE process (the C-ABI a Go caller on this node
+            # would use): rank 0 drives every GPU while the others wait
+            barrier()
+            if rank == 0:
+                try:
+                    out["one_process_multi_gpu"] = one_process_multi_gpu(torch, N, args, world,
+                                                                         bs, dev)
+                except Exception as e:  # reported, never fatal to the bench line
+                    out["one_process_multi_gpu"] = {"error": repr(e)[:500]}
+            barrier()
         if rank == 0:
             out["host_round_trip"] = hrt
             if world == 1:   # the CPU baseline is an N=1 figure (rank 0 only)
                 out["cpu_baseline"] = cpu_baseline(args)
             if args.host_rt_gib > 0:
+                out["config2"] = config2_leg(torch, N, stream, sp)
                 out["small_blobs"] = small_blobs(torch, N, stream, sp)
                 out["config4_end_to_end"] = config4_end_to_end(torch, N, stream, sp)
     if rank == 0:
@@ -297,49 +309,40 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
 
 
 def cpu_baseline(args):
-    """The oracle (a C restatement of the same per-block sequence: keyed
-    BLAKE3, ChaCha20, BLAKE3 CID, ctext into a buffer) timed on host cores over
-    a bounded sample of the same workload (1 MiB blocks of the same stream)."""
+    """The reference's per-block sequence (ref.go:98-161: keyed BLAKE3 DEK,
+    ChaCha20 XOR, BLAKE3 CID of the ctext, ctext into a buffer) timed on host
+    cores over a bounded sample of the same workload (1 MiB blocks of the
+    same stream).  value = the Go path's primitive mix on one core (the
+    reference's Writer is single-goroutine, blob.go:71-83): SIMD BLAKE3
+    (upstream C, AVX-512 -- as lukechampine.com/blake3's assembly, go.mod:12)
+    with a portable scalar ChaCha20 (as x/crypto's generic Go ChaCha20, the
+    one amd64 runs, go.mod:10) -- oracle_post_batch_gomix.  Beside it: the
+    all-scalar oracle port, the all-SIMD libraries (OpenSSL ChaCha20), and
+    the Go mix on all cores of this job over independent block ranges."""
     from oracle import oracle as O
     L = O.lib()
-    n = args.cpu_sample_mib * MIB
-    buf = ctypes.create_string_buffer(n)
-    ct = ctypes.create_string_buffer(n)
-    L.oracle_fill_splitmix(buf, 0, n, args.seed)
-    refs = ctypes.create_string_buffer(64 * -(-n // args.block_size))
-    t = time.perf_counter()
-    L.oracle_post_batch(refs, ct, bytes(32), buf, n, args.block_size, None, 1)
-    dt = time.perf_counter() - t
-    del buf, ct
-    # SURVEY 8(d)(ii): all host cores this job may use, independent block
-    # ranges (the box exports its CPU share as OMP_NUM_THREADS)
     cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(),
                        os.cpu_count()))
-    n2 = 4 * n
-    buf = ctypes.create_string_buffer(n2)
-    ct = ctypes.create_string_buffer(n2)
-    L.oracle_fill_splitmix(buf, 0, n2, args.seed)
-    refs = ctypes.create_string_buffer(64 * -(-n2 // args.block_size))
-    t = time.perf_counter()
-    L.oracle_post_batch(refs, ct, bytes(32), buf, n2, args.block_size, None, cores)
-    dt2 = time.perf_counter() - t
-    # the same blocks on the image's SIMD primitives (upstream BLAKE3 C with
-    # AVX-512, OpenSSL ChaCha20; oracle/cpu_simd.c): closer to what the Go
-    # path's assembly-backed primitives do per core (still not the Go path)
-    simd = None
-    t = time.perf_counter()
-    rc = L.oracle_post_batch_simd(refs, ct, bytes(32), buf, n2, args.block_size, None, 1)
-    dt3 = time.perf_counter() - t
-    if rc == 0:
+    n = args.cpu_sample_mib * MIB
+    n_all = 4 * n
+    buf = ctypes.create_string_buffer(n_all)
+    ct = ctypes.create_string_buffer(n_all)
+    L.oracle_fill_splitmix(buf, 0, n_all, args.seed)
+    refs = ctypes.create_string_buffer(64 * -(-n_all // args.block_size))
+    salt = bytes(32)
+
+    def timed(fn, nbytes, threads):
         t = time.perf_counter()
-        L.oracle_post_batch_simd(refs, ct, bytes(32), buf, n2, args.block_size, None, cores)
-        dt4 = time.perf_counter() - t
-        simd = {"value": round(n2 / GIB / dt3, 4), "cores": 1,
-                "all_cores": {"value": round(n2 / GIB / dt4, 4), "cores": cores},
-                "sample": f"{4 * args.cpu_sample_mib} MiB, oracle_post_batch_simd, "
-                          f"{dt3:.1f} s on 1 thread, {dt4:.1f} s on {cores}",
-                "what": "same per-block sequence on upstream BLAKE3 C (AVX-512) + OpenSSL "
-                        "ChaCha20: an upper bound for the Go path's primitives per core"}
+        rc = fn(refs, ct, salt, buf, nbytes, args.block_size, None, threads)
+        dt = time.perf_counter() - t
+        return (None if rc not in (None, 0) else nbytes / GIB / dt), dt
+
+    go1, dgo1 = timed(L.oracle_post_batch_gomix, n, 1)
+    port_n = max(MIB, n // 3)
+    port1, dport1 = timed(L.oracle_post_batch, port_n, 1)
+    goall, dgoall = timed(L.oracle_post_batch_gomix, n_all, cores)
+    simd1, dsimd1 = timed(L.oracle_post_batch_simd, n, 1)
+    simdall, dsimdall = timed(L.oracle_post_batch_simd, n_all, cores)
     del buf, ct
     model = ""
     try:
@@ -348,18 +351,31 @@ def cpu_baseline(args):
                           if ln.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": round(n / GIB / dt, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+    r4 = lambda v: None if v is None else round(v, 4)
+    if go1 is None:   # no SIMD BLAKE3 in this image: the all-scalar port
+        go1, dgo1, kind_note = port1, dport1, "all-scalar port (no SIMD BLAKE3 found)"
+    else:
+        kind_note = "SIMD BLAKE3 + scalar ChaCha20 (the Go path's primitive mix)"
+    return {"value": r4(go1), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "what": kind_note + ", one thread, same blocks and refs as the GPU",
             "sample": f"{args.cpu_sample_mib} MiB = {n // args.block_size} x "
-                      f"{args.block_size // 1024} KiB blocks, oracle_post_batch, 1 thread, "
-                      f"{dt:.1f} s",
-            "all_cores": {"value": round(n2 / GIB / dt2, 4), "cores": cores,
+                      f"{args.block_size // 1024} KiB blocks, oracle_post_batch_gomix, "
+                      f"1 thread, {dgo1:.1f} s",
+            "all_cores": {"value": r4(goall), "cores": cores,
                           "sample": f"{4 * args.cpu_sample_mib} MiB, {cores} threads over "
-                                    f"independent block ranges, {dt2:.1f} s"},
-            "simd_libraries": simd,
-            "cpu_model": model}
+                                    f"independent block ranges, {dgoall:.1f} s"},
+            "scalar_port": {"value": r4(port1), "cores": 1,
+                            "sample": f"{port_n // MIB} MiB, oracle_post_batch (portable "
+                                      f"scalar BLAKE3 and ChaCha20), {dport1:.1f} s"},
+            "simd_libraries": {"value": r4(simd1), "cores": 1,
+                               "all_cores": {"value": r4(simdall), "cores": cores},
+                               "sample": f"upstream BLAKE3 C (AVX-512) + OpenSSL ChaCha20 "
+                                         f"(AVX-512), {dsimd1:.1f} s / {dsimdall:.1f} s",
+                               "what": "an upper bound for any per-core CPU path"},
+            "nproc": os.cpu_count(), "cpu_model": model}
 
 
-def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=5):
+def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
     """BASELINE config 4's hashing: 1M distinct 4 KiB blobs (glfs.PostBlob with
     the blob type salt, bs = 2 MiB), device-resident, one lane per blob
     (glfsx_post_blobs_device).  Reported beside the headline, not as it."""
@@ -385,11 +401,54 @@ def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=5):
     ms = sum(ts[1:]) / reps
     return {"value": round(n * ln / GIB / (ms * 1e-3), 2), "unit": "GiB/s",
             "blobs_per_s": round(n / (ms * 1e-3)), "ms": round(ms, 3),
+            "reps": reps, "stat": "mean of the reps (HIP events on the launch stream)",
             "what": "1,048,576 distinct 4 KiB blobs, glfs.PostBlob roots (DEK + ChaCha20 "
                     "ctext to HBM + CID), one lane per blob"}
 
 
-def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
+def config2_leg(torch, N, stream, sp, steps=50, warmup=5):
+    """BASELINE configs[1]: a 1 GiB blob at the glfs default block size
+    (2 MiB, glfs.go:12) with the glfs blob type salt (machine.go:50-54, as
+    glfs.PostBlob passes it to bigblob.NewWriter), data = the splitmix stream
+    of seed 1 in HBM, ctext to HBM: 512 data posts + 1 index
+    post per step.  Timed like the headline: HIP events around `steps`
+    back-to-back Creates on the launch stream, mean per step."""
+    from glfs_amd import glfs
+    size, bs = GIB, 2 * MIB
+    salt = glfs.Machine().make_salt("blob")
+    with torch.cuda.stream(stream):
+        data = torch.empty(size, dtype=torch.uint8, device="cuda")
+        ct = torch.empty(size, dtype=torch.uint8, device="cuda")
+        N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), 0, size, 1, sp))
+    stream.synchronize()
+    root, posts = N.glfsx_root(), ctypes.c_uint64()
+
+    def step():
+        N.check(N.lib.glfsx_create_device(bs, salt, None, data.data_ptr(), size,
+                                          ct.data_ptr(), ctypes.byref(root),
+                                          ctypes.byref(posts), sp))
+
+    for _ in range(warmup):
+        step()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    e1.synchronize()
+    wall = (time.perf_counter() - t) / steps
+    ms = e0.elapsed_time(e1) / steps
+    del data, ct
+    return {"value": round(size / GIB / (ms * 1e-3), 2), "unit": "GiB/s",
+            "ms_per_step": round(ms, 4), "wall_ms_per_step": round(wall * 1e3, 4),
+            "steps": steps, "warmup": warmup, "posts_per_step": posts.value,
+            "root_cid": bytes(root.ref)[:32].hex(),
+            "what": "BASELINE configs[1]: 1 GiB blob @ 2 MiB blocks (glfs default), glfs blob "
+                    "salt, splitmix seed 1 in HBM, ctext to HBM; mean over steps (HIP events)"}
+
+
+def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
     """BASELINE config 4 end to end: 1,048,576 distinct 4 KiB blobs (blob i =
     splitmix stream of seed i) posted as glfs blobs (DEK + ChaCha20 ctext to
     HBM + CID per blob, machine.go:64), then the tree of them ("%07d" names,
@@ -446,18 +505,6 @@ def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
                                               offs.data_ptr(), lens.data_ptr(), n, ln,
                                               ct.data_ptr(), roots.data_ptr(), sp))
 
-    def device_route():
-        post_blobs()
-        N.check(N.lib.glfsx_tree_encode_device(n, names.data_ptr(), name_offs.data_ptr(),
-                                               modes.data_ptr(), types.data_ptr(),
-                                               type_offs.data_ptr(), roots.data_ptr(),
-                                               lens.data_ptr(), bss.data_ptr(),
-                                               lines.data_ptr(), lines.numel(), None,
-                                               ctypes.byref(total), sp))
-        N.check(N.lib.glfsx_create_device(bs, tree_salt, None, lines.data_ptr(), total.value,
-                                          tree_ct.data_ptr(), ctypes.byref(root), None, sp))
-        return bytes(root.ref)
-
     def host_route():
         post_blobs()
         with torch.cuda.stream(stream):
@@ -474,27 +521,54 @@ def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
                                    sink, ctypes.byref(counts), ctypes.byref(root)))
         return bytes(root.ref)
 
+    # the device route's pieces, HIP events on the launch stream in the same
+    # reps as its wall time: post_blobs | tree lines | tree Create
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def device_route_timed():
+        ev[0].record(stream)
+        post_blobs()
+        ev[1].record(stream)
+        N.check(N.lib.glfsx_tree_encode_device(n, names.data_ptr(), name_offs.data_ptr(),
+                                               modes.data_ptr(), types.data_ptr(),
+                                               type_offs.data_ptr(), roots.data_ptr(),
+                                               lens.data_ptr(), bss.data_ptr(),
+                                               lines.data_ptr(), lines.numel(), None,
+                                               ctypes.byref(total), sp))
+        ev[2].record(stream)
+        N.check(N.lib.glfsx_create_device(bs, tree_salt, None, lines.data_ptr(), total.value,
+                                          tree_ct.data_ptr(), ctypes.byref(root), None, sp))
+        ev[3].record(stream)
+        return bytes(root.ref)
+
     res = {}
-    for name, fn in (("device", device_route), ("host", host_route)):
+    for name, fn in (("device", device_route_timed), ("host", host_route)):
         fn()
-        ts = []
+        ts, parts = [], []
         for _ in range(reps):
             stream.synchronize()
             t = time.perf_counter()
             r = fn()
             stream.synchronize()
             ts.append(time.perf_counter() - t)
-        sec = min(ts)
+            if name == "device":
+                parts.append([ev[k].elapsed_time(ev[k + 1]) for k in range(3)])
+        sec = sum(ts) / reps
         res[name] = {"value": round(n * ln / GIB / sec, 2), "unit": "GiB/s",
                      "ms": round(sec * 1e3, 3), "blobs_per_s": round(n / sec),
+                     "reps": reps, "stat": "mean wall time over the reps",
+                     "min_ms": round(min(ts) * 1e3, 3),
                      "tree_bytes": total.value, "tree_root_cid": r[:32].hex()}
-    # the device route's pieces (HIP events on the launch stream)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record(stream)
-    post_blobs()
-    ev[1].record(stream)
-    ev[1].synchronize()
-    res["device"]["post_blobs_ms"] = round(ev[0].elapsed_time(ev[1]), 3)
+        if parts:
+            mean = [sum(p[k] for p in parts) / reps for k in range(3)]
+            res[name]["pieces_ms"] = {"post_blobs": round(mean[0], 3),
+                                      "tree_lines": round(mean[1], 3),
+                                      "tree_create": round(mean[2], 3)}
+            res[name]["gpu_ms"] = round(sum(mean), 3)
+            res[name]["host_gaps_ms"] = round(sec * 1e3 - sum(mean), 3)
+            res[name]["pieces_what"] = ("means of HIP events on the launch stream in the same "
+                                        "reps; wall = gpu_ms + host_gaps_ms (launch and sync "
+                                        "overheads between the pieces)")
     assert res["device"]["tree_root_cid"] == res["host"]["tree_root_cid"]
     out = dict(res["device"])
     out["what"] = ("1,048,576 x 4 KiB glfs blobs (HBM) -> roots -> PostTreeMap JSON lines "
@@ -572,6 +646,32 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     res["hashing_store"] = run(store_post, store_ctx(N.GLFSX_STORE_HASH, 0), store_check)
     res["trusting_store_keeping_bytes"] = run(store_post, store_ctx(N.GLFSX_STORE_TRUST, 1),
                                               store_check)
+
+    def io_copy(strict, piece):
+        """Create as bigblob does it: io.Copy(w, r) into the Writer in
+        `piece`-byte writes (glfs.go:53, blob.go:213), pre-hashed store."""
+        best = None
+        for _ in range(3):
+            c = store_ctx(N.GLFSX_STORE_TRUST, 0)()
+            err = ctypes.c_int()
+            barrier()
+            t = time.perf_counter()
+            w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, c, ctypes.byref(err))
+            assert w, N.last_error()
+            N.check(N.lib.glfsx_writer_set_strict(w, int(strict)))
+            rc = N.lib.glfsx_writer_copy(w, host.ctypes.data, n, piece)
+            if rc == 0:
+                rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
+            msg = (N.lib.glfsx_writer_error(w) or b"").decode()
+            N.lib.glfsx_writer_free(w)
+            dt = slowest(time.perf_counter() - t)
+            N.check(rc, msg)
+            store_check(c)
+            best = dt if best is None else min(best, dt)
+        return round(n / GIB / best, 2)
+
+    res["io_copy_32k_pipelined"] = io_copy(False, 32 << 10)
+    res["io_copy_32k_strict"] = io_copy(True, 32 << 10)
     while stores:
         N.lib.glfsx_store_free(stores.pop())
     return {"value": res["trusting_store"], "unit": "GiB/s", "bytes": n,
@@ -587,7 +687,102 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                                  "BLAKE3 on the Writer's thread (ref.go:103 MemStore.Post; "
                                  "upstream BLAKE3 C, AVX-512, 1 core)",
                 "trusting_store_keeping_bytes": "pre-hashed Post into a store that copies "
-                                                "every ctext (MemStore's memory cost)"}}
+                                                "every ctext (MemStore's memory cost)",
+                "io_copy_32k_pipelined": "bigblob.Create as the Go binding runs it by default: "
+                                         "io.Copy's 32 KiB writes (glfs.go:53) into the "
+                                         "Writer, pipelined 64 MiB batches, pre-hashed store",
+                "io_copy_32k_strict": "the same with blob.go:120-133 error timing "
+                                      "(GLFSX_STRICT=1): every Write that completes a block "
+                                      "returns after its Post (one-shot post per block)"}}
+
+
+def one_process_multi_gpu(torch, N, args, world, bs, home):
+    """The multi-GPU write path from ONE process over `world` GPUs (what a
+    Go process on this node calls through the C-ABI): glfsx_create_devices
+    over bf-aligned 16 GiB parts, one per GPU, device-resident (each part's
+    data blocks and level-1 nodes on its GPU, levels >= 2 on the first),
+    and one Writer fed from one pageable host stream with its batches
+    round-robin over every GPU (glfsx_writer_set_devices) into the
+    pre-hashed store."""
+    import numpy as np
+    ndev = torch.cuda.device_count()
+    # one GPU per rank; fewer GPUs than ranks only when rehearsing on one box
+    devs = [k % ndev for k in range(world)]
+    bf = bs // 64
+    part = bs * bf                       # 16 GiB at 1 MiB: one level-1 node
+    bufs = []
+    for k, d in enumerate(devs):
+        N.set_device(d)
+        t = torch.empty(part, dtype=torch.uint8, device=f"cuda:{d}")
+        N.check(N.lib.glfsx_fill_splitmix_device(t.data_ptr(), k * part, part, args.seed, None))
+        bufs.append(t)
+    for d in devs:
+        torch.cuda.synchronize(d)
+    N.set_device(home)
+    nd = len(devs)
+    cdevs = (ctypes.c_int * nd)(*devs)
+    ptrs = (ctypes.c_void_p * nd)(*[t.data_ptr() for t in bufs])
+    sizes = (ctypes.c_uint64 * nd)(*([part] * nd))
+    root, posts = N.glfsx_root(), ctypes.c_uint64()
+
+    def create():
+        N.check(N.lib.glfsx_create_devices(bs, None, None, nd, cdevs, ptrs, sizes, None, None,
+                                           ctypes.byref(root), ctypes.byref(posts)))
+
+    create()
+    reps = 5
+    t = time.perf_counter()
+    for _ in range(reps):
+        create()
+    sec = (time.perf_counter() - t) / reps
+    dev_res = {"value": round(nd * part / GIB / sec, 2), "unit": "GiB/s",
+               "ms_per_create": round(sec * 1e3, 3), "gpus": nd, "part_bytes": part,
+               "posts": posts.value, "root_cid": bytes(root.ref)[:32].hex(),
+               "what": f"glfsx_create_devices, {nd} x {part // GIB} GiB parts in HBM "
+                       "(ctext not written), mean of 5 Creates, host wall clock"}
+    del bufs
+    # one host stream over all GPUs
+    per = int(min(args.host_rt_gib, 4.0) * GIB) // bs * bs
+    host_res = None
+    if per > 0:
+        n = per * nd
+        host = np.empty(n, dtype=np.uint8)
+        tmp = torch.empty(64 * MIB, dtype=torch.uint8, device=f"cuda:{home}")
+        for off in range(0, n, 64 * MIB):
+            m = min(64 * MIB, n - off)
+            N.check(N.lib.glfsx_fill_splitmix_device(tmp.data_ptr(), off, m, args.seed, None))
+            torch.cuda.synchronize()
+            host[off:off + m] = tmp[:m].cpu().numpy()
+        del tmp
+        store_post = ctypes.cast(N.lib.glfsx_store_post, N.POST_FN)
+        best = {}
+        for label, lanes in (("one_gpu", devs[:1]), ("all_gpus", devs)):
+            for _ in range(3):
+                st = N.lib.glfsx_store_new(bs, N.GLFSX_STORE_TRUST, 0, 0, None)
+                err = ctypes.c_int()
+                t = time.perf_counter()
+                w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, st, ctypes.byref(err))
+                assert w, N.last_error()
+                rc = N.lib.glfsx_writer_set_devices(w, (ctypes.c_int * len(lanes))(*lanes),
+                                                    len(lanes))
+                if rc == 0:
+                    rc = N.lib.glfsx_writer_copy(w, host.ctypes.data, n, 64 * MIB)
+                if rc == 0:
+                    rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
+                msg = (N.lib.glfsx_writer_error(w) or b"").decode()
+                N.lib.glfsx_writer_free(w)
+                dt = time.perf_counter() - t
+                N.lib.glfsx_store_free(st)
+                N.check(rc, msg)
+                best[label] = min(best.get(label, dt), dt)
+        host_res = {"value": round(n / GIB / best["all_gpus"], 2), "unit": "GiB/s",
+                    "one_gpu_value": round(n / GIB / best["one_gpu"], 2), "bytes": n,
+                    "root_cid": bytes(root.ref)[:32].hex(),
+                    "what": f"one Writer, one pageable host stream of {n // GIB} GiB in 64 MiB "
+                            f"writes, batches round-robin over {nd} GPUs (glfsx_writer_set_"
+                            "devices), pre-hashed store; one_gpu_value: the same on the first "
+                            "GPU only; best of 3"}
+    return {"device_resident": dev_res, "host_stream": host_res}
 
 
 def postblob_latency(N, calls=300):

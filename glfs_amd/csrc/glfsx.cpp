@@ -1495,20 +1495,23 @@ int drain(glfsx_writer *w) {
   return complete_all(w);
 }
 
-// Finish with a few complete blocks (<= kFewBlocks) and the tail staged on
-// the host: they go out as one coalesced one-shot post (a request per block)
-// instead of a batch through the three-stream pipeline, so a PostBlob of a
-// few MiB is one launch pair and one wait.  Posts and addRef replay in block
-// order (blob.go:152-163), after every older batch's.
+// A few complete blocks (<= kFewBlocks) staged on the host -- with the tail
+// at Finish, or without it in a strict Write -- go out as one coalesced
+// one-shot post (a request per block, the kernels reading the pinned
+// staging in place) instead of a batch through the three-stream pipeline:
+// a PostBlob of a few MiB, or a strict Write that completes a block, is one
+// launch pair and one wait.  Posts and addRef replay in block order
+// (blob.go:152-163), after every older batch's.  Without the tail, the
+// partial block's bytes move to the front of the staging.
 constexpr uint64_t kFewBlocks = 8;
-int finish_few(glfsx_writer *w, bool *done) {
+int post_few(glfsx_writer *w, bool tail, bool *done) {
   *done = false;
   WSlot &sl = w->slot[w->cur];
   if (!one_enabled() || sl.on_dev || w->full == 0 || w->full > kFewBlocks ||
       w->bs > kMaxMedLen || (w->bs & 15) || !sl.h_in.dp)
     return 0;
   if (int e = complete_all(w)) return e;
-  const uint64_t k = w->full + (w->partial ? 1 : 0);
+  const uint64_t k = w->full + (tail && w->partial ? 1 : 0);
   OneBuf &o = w->one;
   if (w->post)
     if (int e = o.h_ct.ensure(w->full * w->bs + w->partial + 64)) return e;
@@ -1539,10 +1542,21 @@ int finish_few(glfsx_writer *w, bool *done) {
     if (int e = add_ref(w, 0, &refs[64 * b])) return e;
     w->size += len;
   }
+  if (tail)
+    w->partial = 0;
+  else if (w->partial)
+    memmove(sl.h_in.u8(), sl.h_in.u8() + w->full * w->bs, w->partial);
   w->full = 0;
-  w->partial = 0;
   *done = true;
   return 0;
+}
+
+// blob.go:120-133 error timing: deliver the Posts of every block completed
+// so far before the Write returns.
+int drain_strict(glfsx_writer *w) {
+  bool few = false;
+  if (int e = post_few(w, false, &few)) return e;
+  return few ? complete_all(w) : drain(w);
 }
 }  // namespace
 
@@ -1570,7 +1584,16 @@ int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
       if (int e = submit(w)) return call.done(w->sticky = e);
   }
   if (w->strict)
-    if (int e = drain(w)) return call.done(w->sticky = e);
+    if (int e = drain_strict(w)) return call.done(w->sticky = e);
+  return 0;
+}
+
+int glfsx_writer_copy(glfsx_writer *w, const void *data, uint64_t n, uint64_t piece) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  if (piece == 0) return fail(GLFSX_E_ARG, "piece of 0 bytes");
+  const uint8_t *p = static_cast<const uint8_t *>(data);
+  for (uint64_t off = 0; off < n; off += piece)
+    if (int e = glfsx_writer_write(w, p + off, std::min(piece, n - off))) return e;
   return 0;
 }
 
@@ -1677,7 +1700,7 @@ int glfsx_writer_finish(glfsx_writer *w, glfsx_root *out) {
   WriterCall call(w);
   if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
   bool few = false;
-  if (int e = finish_few(w, &few)) return call.done(w->sticky = e);
+  if (int e = post_few(w, true, &few)) return call.done(w->sticky = e);
   if (!few)
     if (int e = drain(w)) return call.done(w->sticky = e);
   if (w->partial) {  // blob.go:136-140: the tail block, never padded

@@ -186,6 +186,10 @@ int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
  * side fused with its Writer. */
 int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
                              uint64_t block_size, const uint8_t *refs);
+/* io.Copy(w, r) (blob.go:213, glfs.go:53) from an in-memory reader: n bytes
+ * in glfsx_writer_write calls of `piece` bytes each (io.Copy's 32 KiB
+ * buffer for a reader without WriterTo), stopping at the first error. */
+int glfsx_writer_copy(glfsx_writer *w, const void *data, uint64_t n, uint64_t piece);
 /* Deliver the Posts of every complete block written so far (no reference
  * counterpart: the reference never holds a complete block back). */
 int glfsx_writer_flush(glfsx_writer *w);

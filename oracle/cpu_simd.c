@@ -14,6 +14,12 @@
  * bound on what the Go path's primitives can do per core, not the Go path.
  * Both libraries are loaded with dlopen; when either is absent the function
  * returns -1.
+ *
+ * oracle_post_batch_gomix is the Go path's primitive mix instead: the same
+ * SIMD BLAKE3 for the DEK and the CID (as lukechampine's AVX-512 assembly,
+ * go.mod:12) with the portable scalar ChaCha20 of oracle.c (as x/crypto's
+ * generic Go ChaCha20, the one amd64 runs, go.mod:10; ref.go:137-144).
+ * bench.py reports it as cpu_baseline.value.
  */
 #include <dlfcn.h>
 #include <pthread.h>
@@ -59,6 +65,7 @@ typedef struct {
   uint8_t *refs, *ctext;
   const uint8_t *salt, *ptext, *cid_key;
   uint64_t total, chunk, b0, b1;
+  int scalar_chacha;
   int rc;
 } job;
 
@@ -78,8 +85,11 @@ static void *run(void *arg) {
     L->update(h, j->ptext + off, n);
     L->finalize(h, ref + 32, 32);
     int outl = 0; /* ctext: ref.go:137-144 */
-    if (L->enc_init(cx, L->chacha(), NULL, ref + 32, iv) != 1 ||
-        (n && L->enc_update(cx, ct, &outl, j->ptext + off, (int)n) != 1)) {
+    if (j->scalar_chacha) {
+      static const uint8_t zero_nonce[12] = {0};
+      oracle_chacha20_xor(ct, j->ptext + off, n, ref + 32, zero_nonce, 0);
+    } else if (L->enc_init(cx, L->chacha(), NULL, ref + 32, iv) != 1 ||
+               (n && L->enc_update(cx, ct, &outl, j->ptext + off, (int)n) != 1)) {
       j->rc = -1;
       break;
     }
@@ -96,9 +106,9 @@ static void *run(void *arg) {
   return NULL;
 }
 
-int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
-                           const uint8_t *ptext, uint64_t total, uint64_t chunk,
-                           const uint8_t *cid_key, int threads) {
+static int post_batch(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
+                      const uint8_t *ptext, uint64_t total, uint64_t chunk,
+                      const uint8_t *cid_key, int threads, int scalar_chacha) {
   static simd_libs L;
   static int loaded = 0;
   if (!loaded) loaded = load(&L) == 0 ? 1 : -1;
@@ -110,7 +120,7 @@ int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32]
   for (int t = 0; t < threads; t++) {
     jobs[t] = (job){&L, refs, ctext, salt, ptext, cid_key, total, chunk,
                     nb * (uint64_t)t / (uint64_t)threads,
-                    nb * (uint64_t)(t + 1) / (uint64_t)threads, 0};
+                    nb * (uint64_t)(t + 1) / (uint64_t)threads, scalar_chacha, 0};
     pthread_create(&th[t], NULL, run, &jobs[t]);
   }
   int rc = 0;
@@ -121,4 +131,16 @@ int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32]
   free(jobs);
   free(th);
   return rc;
+}
+
+int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
+                           const uint8_t *ptext, uint64_t total, uint64_t chunk,
+                           const uint8_t *cid_key, int threads) {
+  return post_batch(refs, ctext, salt, ptext, total, chunk, cid_key, threads, 0);
+}
+
+int oracle_post_batch_gomix(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
+                            const uint8_t *ptext, uint64_t total, uint64_t chunk,
+                            const uint8_t *cid_key, int threads) {
+  return post_batch(refs, ctext, salt, ptext, total, chunk, cid_key, threads, 1);
 }

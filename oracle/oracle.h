@@ -106,6 +106,11 @@ void oracle_post_batch(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
 int oracle_post_batch_simd(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
                            const uint8_t *ptext, uint64_t total, uint64_t chunk,
                            const uint8_t *cid_key, int threads);
+/* The Go path's primitive mix (cpu_simd.c): SIMD BLAKE3 for DEK and CID,
+ * the portable scalar ChaCha20 above.  Returns -1 when BLAKE3 is missing. */
+int oracle_post_batch_gomix(uint8_t *refs, uint8_t *ctext, const uint8_t salt[32],
+                            const uint8_t *ptext, uint64_t total, uint64_t chunk,
+                            const uint8_t *cid_key, int threads);
 
 /* Deterministic data generator shared by tests/bench: byte offset o ->
  * byte (o & 7) of splitmix64(seed ^ (o >> 3)), little-endian. */

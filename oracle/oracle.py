@@ -55,6 +55,7 @@ def lib():
         L.oracle_post_batch_simd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_u8p,
                                              ctypes.c_void_p, ctypes.c_uint64,
                                              ctypes.c_uint64, c_u8p, ctypes.c_int]
+        L.oracle_post_batch_gomix.argtypes = L.oracle_post_batch_simd.argtypes
         L.oracle_fill_splitmix.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
                                            ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_fill_splitmix_blobs.argtypes = [ctypes.c_void_p, ctypes.c_uint64,

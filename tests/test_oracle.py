@@ -166,3 +166,7 @@ def test_simd_cpu_baseline_same_refs(O):
     if rc == -1:
         pytest.skip("libclang-cpp BLAKE3 or libcrypto absent")
     assert a.raw == b.raw and ca.raw == cb.raw
+    # the Go path's mix (SIMD BLAKE3 + scalar ChaCha20): bench's cpu_baseline.value
+    g, cg = ctypes.create_string_buffer(64 * nb), ctypes.create_string_buffer(n)
+    assert L.oracle_post_batch_gomix(g, cg, salt, data, n, bs, None, 2) == 0
+    assert a.raw == g.raw and ca.raw == cg.raw
