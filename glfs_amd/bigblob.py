@@ -77,8 +77,8 @@ def _salt_arg(salt: Optional[bytes]) -> Optional[bytes]:
 def derive_key(salt: bytes, data: bytes, out_len: int = 32) -> bytes:
     """ref.go:152-161 DeriveKey(out, salt, input): BLAKE3 keyed with salt,
     first out_len XOF bytes (GPU)."""
-    out = ctypes.create_string_buffer(32)
-    data = bytes(data)
+    out = ctypes.create_string_buffer(max(out_len, 1))
+    data = data if isinstance(data, (bytes, memoryview)) else bytes(data)
     N.check(N.lib.glfsx_derive_key(out, out_len, _salt_arg(salt), data, len(data)))
     return out.raw[:out_len]
 

@@ -457,6 +457,41 @@ int derive_key_dev(Ctx *c, uint8_t out[32], const uint8_t salt[32],
   return 0;
 }
 
+// DeriveKey's full contract (ref.go:152-161): any input length, any output
+// length -- the streaming one-workgroup hasher of xof_kernels.hip, input in
+// slabs of 256 MiB through device staging.
+int derive_key_xof(Ctx *c, uint8_t *out, size_t out_len, const uint8_t salt[32],
+                   const void *in, size_t n) {
+  constexpr uint64_t kGroup = 256ull << 10, kSlabGroups = 1024;
+  if (int e = c->d_small.ensure(sizeof(B3State) + out_len + 64)) return e;
+  if (int e = c->d_in.ensure(std::min<uint64_t>(n, kSlabGroups * kGroup) + 64)) return e;
+  B3State h{};
+  words_from_key(h.key, salt);
+  h.base = 16;  // KEYED_HASH (BLAKE3 spec 2.1)
+  auto *st = reinterpret_cast<B3State *>(c->d_small.p);
+  uint8_t *d_out = c->d_small.u8() + ((sizeof(B3State) + 63) & ~size_t(63));
+  HIP_TRY(hipMemcpyAsync(st, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+  const uint8_t *p = static_cast<const uint8_t *>(in);
+  // every whole group that does not hold the last byte
+  const uint64_t groups = n ? (n - 1) / kGroup : 0;
+  for (uint64_t g0 = 0; g0 < groups; g0 += kSlabGroups) {
+    const uint64_t k = std::min(kSlabGroups, groups - g0);
+    HIP_TRY(hipMemcpyAsync(c->d_in.p, p + g0 * kGroup, k * kGroup, hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(launch_b3_absorb(st, c->d_in.u8(), k, c->stream));
+  }
+  const uint64_t rem = n - groups * kGroup;
+  if (rem)
+    HIP_TRY(hipMemcpyAsync(c->d_in.p, p + groups * kGroup, rem, hipMemcpyHostToDevice,
+                           c->stream));
+  HIP_TRY(launch_b3_final(st, c->d_in.u8(), rem, d_out, out_len, c->stream));
+  std::vector<uint8_t> tmp(out_len);
+  HIP_TRY(hipMemcpyAsync(tmp.data(), d_out, out_len, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(stream_wait(c->stream));
+  memcpy(out, tmp.data(), out_len);
+  return 0;
+}
+
 int check_block_size(uint64_t bs) {
   if (bs < GLFSX_MIN_BLOCK_SIZE)
     return fail(GLFSX_E_BLOCKSIZE_LT_MIN, "blockSize cannot be < %d",
@@ -1179,11 +1214,12 @@ int glfsx_set_device(int dev) {
 
 int glfsx_derive_key(uint8_t *out, size_t out_len, const uint8_t salt[32],
                      const void *input, size_t n) {
-  if (!out || !salt || (n && !input)) return fail(GLFSX_E_ARG, "null argument");
-  if (out_len > 32)
-    return fail(GLFSX_E_UNSUPPORTED, "derive_key out_len %zu > 32", out_len);
+  if ((out_len && !out) || !salt || (n && !input)) return fail(GLFSX_E_ARG, "null argument");
+  if (out_len == 0) return 0;
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
+  if (out_len > 32 || n > kMaxMsgLen)
+    return derive_key_xof(c, static_cast<uint8_t *>(out), out_len, salt, input, n);
   uint8_t full[32];
   if (int e = derive_key_dev(c, full, salt, input, n)) return e;
   memcpy(out, full, out_len);

@@ -161,6 +161,23 @@ hipError_t launch_fill_blobs(uint8_t *dst, uint64_t n, uint64_t len, uint64_t se
 hipError_t debug_wgtime(uint64_t *out);  // 8192 x 8 words (diagnostic builds)
 #endif
 
+// DeriveKey of any input length and output length (xof_kernels.hip): the
+// hash state of one stream, carried across launches in device memory.
+struct B3State {
+  uint32_t key[8];
+  uint32_t base;    // flags of every compression (kKeyed for DeriveKey)
+  uint32_t depth;   // entries on the CV stack
+  uint64_t chunks;  // chunks absorbed (a multiple of 256)
+  uint32_t stack[64][8];
+};
+// `groups` whole 256-chunk groups at src, none of them holding the input's
+// last byte.
+hipError_t launch_b3_absorb(B3State *st, const uint8_t *src, uint64_t groups, hipStream_t s);
+// The input's last n bytes (<= 256 KiB; 0 only for the empty input), then
+// out_len bytes of XOF output.
+hipError_t launch_b3_final(B3State *st, const uint8_t *src, uint64_t n, uint8_t *out,
+                           uint64_t out_len, hipStream_t s);
+
 void words_from_key(uint32_t w[8], const uint8_t key[32]);
 void blake3_iv_words(uint32_t w[8]);
 

@@ -117,8 +117,9 @@ uint32_t glfsx_set_latency_wgs(uint32_t wgs);
 uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);
 
 /* --- primitives -------------------------------------------------------- */
-/* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input, first out_len
- * (<= 32) bytes of the XOF. */
+/* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input (any length),
+ * the first out_len bytes of the XOF (any length; blake3.New(len(out), salt)
+ * then h.XOF() and io.ReadFull).  out_len 0 writes nothing. */
 int glfsx_derive_key(uint8_t *out, size_t out_len, const uint8_t salt[32],
                      const void *input, size_t n);
 

@@ -829,3 +829,38 @@ def test_post_blobs_mixed_sizes(gpu, O):
         assert rh[64 * i:64 * i + 64] == refs[i].root.ref.marshal_binary(), i
         if 0 < len(b) <= bs:
             assert cth[offs[i]:offs[i] + len(b)] == O.post(O.derive_key(blob_salt, b"raw"), b)[1]
+
+
+def test_derive_key_xof_any_length(gpu, O):
+    """ref.go:152-161 with len(out) > 32 (the XOF beyond the digest: output
+    blocks 0, 1, ... of the root node) and with inputs that take the
+    streaming hasher: every byte vs the oracle's XOF, which
+    tests/test_oracle.py pins against upstream BLAKE3 C."""
+    from glfs_amd import bigblob
+    rng = random.Random(9)
+    salt = bytes(rng.randrange(256) for _ in range(32))
+    for n in [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 5000, 256 * 1024 - 1, 256 * 1024,
+              256 * 1024 + 1, 3 * 256 * 1024 + 4097, 1 << 22]:
+        data = O.fill_splitmix(n, n + 3)
+        for out_len in (33, 64, 65, 131, 1000):
+            assert bigblob.derive_key(salt, data, out_len) == O.blake3(data, salt, out_len), \
+                (n, out_len)
+        # the first 32 bytes equal the digest path's
+        assert bigblob.derive_key(salt, data, 40)[:32] == bigblob.derive_key(salt, data), n
+
+
+def test_derive_key_input_above_4gib(gpu, O):
+    """An input longer than the write path's 4 GiB message limit: 4 GiB +
+    1 MiB + 5 bytes through the streaming hasher (17 slabs), 32 and 100 bytes
+    of output vs the oracle (threaded over the chunks is not available for a
+    single keyed message, so the reference is upstream BLAKE3 C when the
+    image has it, else the oracle)."""
+    import refimpl as R
+    from glfs_amd import bigblob
+    n = (4 << 30) + (1 << 20) + 5
+    data = O.fill_splitmix(n, 77)
+    salt = bytes(range(32))
+    want = (R.blake3(data, salt, 100) if R.blake3_lib() is not None
+            else O.blake3(data, salt, 100))
+    assert bigblob.derive_key(salt, data, 100) == want
+    assert bigblob.derive_key(salt, data, 32) == want[:32]
