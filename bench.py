@@ -670,8 +670,41 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
             best = dt if best is None else min(best, dt)
         return round(n / GIB / best, 2)
 
+    def read_from(piece):
+        """io.Copy through the Writer's ReadFrom (glfsx_writer_reserve /
+        _commit): a reader that copies up to `piece` bytes per Read straight
+        into the pinned staging (one thread, like read(2) from a file)."""
+        best = None
+        buf, cap = ctypes.c_void_p(), ctypes.c_uint64()
+        for _ in range(3):
+            c = store_ctx(N.GLFSX_STORE_TRUST, 0)()
+            err = ctypes.c_int()
+            barrier()
+            t = time.perf_counter()
+            w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, c, ctypes.byref(err))
+            assert w, N.last_error()
+            off, rc = 0, 0
+            while rc == 0 and off < n:
+                rc = N.lib.glfsx_writer_reserve(w, ctypes.byref(buf), ctypes.byref(cap))
+                if rc == 0:
+                    k = min(cap.value, piece, n - off)
+                    ctypes.memmove(buf.value, host.ctypes.data + off, k)
+                    rc = N.lib.glfsx_writer_commit(w, k)
+                    off += k
+            if rc == 0:
+                rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
+            msg = (N.lib.glfsx_writer_error(w) or b"").decode()
+            N.lib.glfsx_writer_free(w)
+            dt = slowest(time.perf_counter() - t)
+            N.check(rc, msg)
+            store_check(c)
+            best = dt if best is None else min(best, dt)
+        return round(n / GIB / best, 2)
+
     res["io_copy_32k_pipelined"] = io_copy(False, 32 << 10)
     res["io_copy_32k_strict"] = io_copy(True, 32 << 10)
+    res["read_from_1m"] = read_from(MIB)
+    res["read_from_64m"] = read_from(64 * MIB)
     while stores:
         N.lib.glfsx_store_free(stores.pop())
     return {"value": res["trusting_store"], "unit": "GiB/s", "bytes": n,
@@ -688,12 +721,17 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                                  "upstream BLAKE3 C, AVX-512, 1 core)",
                 "trusting_store_keeping_bytes": "pre-hashed Post into a store that copies "
                                                 "every ctext (MemStore's memory cost)",
-                "io_copy_32k_pipelined": "bigblob.Create as the Go binding runs it by default: "
-                                         "io.Copy's 32 KiB writes (glfs.go:53) into the "
-                                         "Writer, pipelined 64 MiB batches, pre-hashed store",
+                "io_copy_32k_pipelined": "bigblob.Create fed by io.Copy's 32 KiB Writes "
+                                         "(glfs.go:53; a reader that is not a WriterTo, "
+                                         "into a Writer without ReadFrom), pipelined 64 MiB "
+                                         "batches, pre-hashed store",
                 "io_copy_32k_strict": "the same with blob.go:120-133 error timing "
                                       "(GLFSX_STRICT=1): every Write that completes a block "
-                                      "returns after its Post (one-shot post per block)"}}
+                                      "returns after its Post (one-shot post per block)",
+                "read_from_1m": "io.Copy through the Writer's ReadFrom (glfsx_writer_reserve"
+                                "/_commit): the reader copies 1 MiB per Read straight into "
+                                "the pinned staging (one thread, no second copy)",
+                "read_from_64m": "the same with 64 MiB Reads"}}
 
 
 def one_process_multi_gpu(torch, N, args, world, bs, home):

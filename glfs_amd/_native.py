@@ -76,6 +76,9 @@ SIGNATURES = {
     "glfsx_writer_write": (_INT, [_VP, _VP, _SZ]),
     "glfsx_writer_flush": (_INT, [_VP]),
     "glfsx_writer_copy": (_INT, [_VP, _VP, _U64, _U64]),
+    "glfsx_writer_reserve": (_INT, [_VP, ctypes.POINTER(ctypes.c_void_p),
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+    "glfsx_writer_commit": (_INT, [_VP, _U64]),
     "glfsx_writer_write_device": (_INT, [_VP, _VP, _SZ, _VP]),
     "glfsx_writer_write_ctext": (_INT, [_VP, _VP, _U64, _U64, _VP]),
     "glfsx_writer_set_strict": (_INT, [_VP, _INT]),

@@ -181,6 +181,25 @@ class Writer:
             self._raise(rc)
         return n
 
+    def read_from(self, r) -> int:
+        """io.ReaderFrom (io.Copy in Create/Concat, blob.go:213,341, uses it):
+        r.readinto() straight into the writer's pinned staging
+        (glfsx_writer_reserve / glfsx_writer_commit), no second copy."""
+        total = 0
+        buf, cap = ctypes.c_void_p(), ctypes.c_uint64()
+        while True:
+            rc = N.lib.glfsx_writer_reserve(self._w, ctypes.byref(buf), ctypes.byref(cap))
+            if rc:
+                self._raise(rc)
+            view = (ctypes.c_char * cap.value).from_address(buf.value)
+            n = r.readinto(memoryview(view).cast("B")) or 0
+            rc = N.lib.glfsx_writer_commit(self._w, n)
+            if rc:
+                self._raise(rc)
+            total += n
+            if n == 0:
+                return total
+
     def finish(self) -> Root:
         """blob.go:135-150."""
         r = N.glfsx_root()
@@ -203,9 +222,13 @@ class Writer:
 
 def _copy(w, r: Union[bytes, bytearray, memoryview, BinaryIO]) -> None:
     """io.Copy: a bytes-like source is one Write (bytes.Reader is a WriterTo);
-    a stream is copied in 32 KiB pieces."""
+    a stream with readinto goes through the Writer's ReadFrom (read straight
+    into the staging), any other stream in 32 KiB pieces."""
     if isinstance(r, (bytes, bytearray, memoryview)):
         w.write(r)
+        return
+    if hasattr(r, "readinto"):
+        w.read_from(r)
         return
     while True:
         piece = r.read(32 * 1024)

@@ -187,6 +187,16 @@ int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
  * side fused with its Writer. */
 int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
                              uint64_t block_size, const uint8_t *refs);
+/* A Writer's io.ReaderFrom (no reference counterpart; io.Copy in Create and
+ * Concat, blob.go:213,341, uses it when the Writer has it): reserve lends
+ * the caller the next *cap >= 1 bytes of the writer's pinned staging at
+ * *buf, the caller reads up to that many bytes of input into it (r.Read),
+ * and commit(n) takes the first n as if glfsx_writer_write(buf, n) had been
+ * called -- the input is copied once, by the reader, instead of into a
+ * 32 KiB buffer and again into staging.  No other call on the writer
+ * between the two; the area is the writer's again after commit. */
+int glfsx_writer_reserve(glfsx_writer *w, void **buf, uint64_t *cap);
+int glfsx_writer_commit(glfsx_writer *w, uint64_t n);
 /* io.Copy(w, r) (blob.go:213, glfs.go:53) from an in-memory reader: n bytes
  * in glfsx_writer_write calls of `piece` bytes each (io.Copy's 32 KiB
  * buffer for a reader without WriterTo), stopping at the first error. */

@@ -67,6 +67,7 @@ import (
 	"context"
 	"errors"
 	"fmt"
+	"io"
 	"os"
 	"runtime/cgo"
 	"strconv"
@@ -191,6 +192,33 @@ func (gw *gpuWriter) Write(data []byte) (int, error) {
 		return 0, gw.fail(rc)
 	}
 	return len(data), nil
+}
+
+// ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341): the
+// reader fills the writer's pinned staging directly (glfsx_writer_reserve /
+// glfsx_writer_commit), so every byte is copied once, by r.Read, instead of
+// into io.Copy's 32 KiB buffer and again by Write.  C memory handed to Go as
+// a slice is fine under the cgo rules; it is not used after commit.
+func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
+	var total int64
+	for {
+		var p unsafe.Pointer
+		var room C.uint64_t
+		if rc := C.glfsx_writer_reserve(gw.w, &p, &room); rc != 0 {
+			return total, gw.fail(rc)
+		}
+		n, err := r.Read(unsafe.Slice((*byte)(p), int(room)))
+		if rc := C.glfsx_writer_commit(gw.w, C.uint64_t(n)); rc != 0 {
+			return total + int64(n), gw.fail(rc)
+		}
+		total += int64(n)
+		if err == io.EOF {
+			return total, nil
+		}
+		if err != nil {
+			return total, err
+		}
+	}
 }
 
 // Finish mirrors blob.go:135-150.

@@ -8,6 +8,7 @@ package bigblob
 
 import (
 	"context"
+	"io"
 
 	"blobcache.io/blobcache/src/bcsdk"
 )
@@ -15,6 +16,7 @@ import (
 type gpuWriter struct{ ctx context.Context }
 
 func (gw *gpuWriter) Write([]byte) (int, error)             { panic("unreachable") }
+func (gw *gpuWriter) ReadFrom(io.Reader) (int64, error)     { panic("unreachable") }
 func (gw *gpuWriter) Finish(context.Context) (*Root, error) { panic("unreachable") }
 
 func (ag *Machine) newGPUWriter(bcsdk.WO, *[32]byte) *Writer { return nil }

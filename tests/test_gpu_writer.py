@@ -232,3 +232,72 @@ def test_concat_write_ctext_vs_oracle(gpu, O):
     assert got.ref.marshal_binary() == want
     assert got.size == sum(map(len, parts))
     assert bigblob.read_all(st, got) == b"".join(parts)
+
+
+class _ChunkyReader:
+    """An io.Reader whose Reads return random amounts (1 B .. 3 MiB), read
+    into the caller's buffer (readinto), like a pipe or socket."""
+
+    def __init__(self, data, seed):
+        self.data, self.off = memoryview(data), 0
+        self.rng = random.Random(seed)
+
+    def readinto(self, buf):
+        n = min(len(buf), len(self.data) - self.off, self.rng.choice([1, 4096, 65536, 1 << 20,
+                                                                     3 << 20, 777_777]))
+        buf[:n] = self.data[self.off:self.off + n]
+        self.off += n
+        return n
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_read_from_vs_oracle(gpu, O, strict):
+    """Writer.ReadFrom (glfsx_writer_reserve / _commit: the reader fills the
+    pinned staging, io.Copy's fast path in Create): the Post log (kind,
+    ref, ctext) and root equal the oracle writer's, with Reads of random
+    sizes, pipelined and strict."""
+    from glfs_amd import bigblob
+    bs = 1 << 20
+    data = O.fill_splitmix(70 * bs + 4321, 31)
+    want_root, _, _, want = O.create(data, bs)
+    st = bigblob.MemStore(bs)
+    w = bigblob.Machine(bs).new_writer(st, None, strict=strict)
+    try:
+        assert w.read_from(_ChunkyReader(data, 5)) == len(data)
+        root = w.finish()
+    finally:
+        w.close()
+    assert root.ref.marshal_binary() == want_root and root.size == len(data)
+    assert [(k, r) for k, r, _ in st.log] == [(k, r) for k, r, _, _ in want]
+    for (k, r, n), (_, _, _, ct) in zip(st.log, want):
+        assert st.blobs[r[:32]] == ct
+
+
+def test_read_from_store_error(gpu, O):
+    """A store error during ReadFrom: raised, and the Posts delivered are the
+    reference's prefix (no Post after the failing one)."""
+    from glfs_amd import bigblob
+    bs = 4096
+    data = O.fill_splitmix(200 * bs + 5, 37)
+    _, want_posts = _oracle_fail_run(O, data, bs, [len(data)], 90)
+    st = _FailingStore(bs, 90)
+    w = bigblob.Machine(bs).new_writer(st, None, strict=True)
+    with pytest.raises(bigblob.StoreError):
+        w.read_from(_ChunkyReader(data, 7))
+        w.finish()
+    w.close()
+    assert [(k, r) for k, r, _ in st.inner.log] == want_posts
+
+
+def test_commit_more_than_reserved_fails(gpu):
+    N = gpu
+    err = ctypes.c_int()
+    w = N.lib.glfsx_writer_new(1 << 20, 1 << 20, None, None, N.POST_FN(0), None,
+                               ctypes.byref(err))
+    try:
+        buf, cap = ctypes.c_void_p(), ctypes.c_uint64()
+        assert N.lib.glfsx_writer_reserve(w, ctypes.byref(buf), ctypes.byref(cap)) == 0
+        assert cap.value == 64 << 20 and buf.value
+        assert N.lib.glfsx_writer_commit(w, cap.value + 1) == N.GLFSX_E_ARG
+    finally:
+        N.lib.glfsx_writer_free(w)

@@ -42,6 +42,7 @@ def test_patch_hooks_exist_in_both_builds():
     assert "ag.newGPUWriter(s, salt)" in added
     assert "w.gpu.Write(data)" in added and "w.gpu.Finish(ctx)" in added
     assert "w.gpu.ctx = ctx" in added and "gpu *gpuWriter" in added
+    assert "return w.gpu.ReadFrom(r)" in added and "io.Copy(writerOnly{w}, r)" in added
     # context lines are the reference's own (blob.go:85-86)
     assert " func (ag *Machine) NewWriter(s bcsdk.WO, salt *[32]byte) *Writer {" in patch
     assert " \tblockSize := s.MaxSize()" in patch
@@ -55,6 +56,8 @@ def test_patch_hooks_exist_in_both_builds():
         assert re.search(r"func \(gw \*gpuWriter\) Write\((data )?\[\]byte\) \(int, error\)", src), name
         assert re.search(r"func \(gw \*gpuWriter\) Finish\((ctx )?context\.Context\) "
                          r"\(\*Root, error\)", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) ReadFrom\((r )?io\.Reader\) "
+                         r"\(int64, error\)", src), name
         assert "schema.WO" not in src, name
         assert src.count("{") == src.count("}"), name
         assert src.count("(") == src.count(")"), name
