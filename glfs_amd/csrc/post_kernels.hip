@@ -1830,12 +1830,11 @@ struct SArgs {
   uint32_t out_off;
 };
 
-template <int G, bool CHACHA, int A = 2>
-__global__ __launch_bounds__(256) void k_small(SArgs a) {
-  // 4 waves x 8 KiB staging image (same layout as k_pass's)
-  __shared__ uint4 lds_u4[4 * 512];
-  const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
-  if (i >= a.n) return;  // no barriers in this kernel
+// Blob i for the calling lane (nothing when i >= n); lds_u4: the
+// workgroup's 4 x 8 KiB staging images.  No barriers.
+template <int G, bool CHACHA, int A>
+__device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *lds_u4) {
+  if (i >= a.n) return;
   const uint64_t off = a.offs[i], len = a.lens[i];
   if (len > kMaxSmallLen) return;  // posted by the host's large-blob route
   const uint8_t *msg = a.src + off;
@@ -1877,6 +1876,40 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
     lane_subtree<G, CHACHA, false, A>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
   }
   store_digest(ref + a.out_off, cv);
+}
+
+template <int G, bool CHACHA, int A = 2>
+__global__ __launch_bounds__(256) void k_small(SArgs a) {
+  // 4 waves x 8 KiB staging image (same layout as k_pass's)
+  __shared__ uint4 lds_u4[4 * 512];
+  small_blob<G, CHACHA, A>(a, blockIdx.x * uint64_t(blockDim.x) + threadIdx.x, lds_u4);
+}
+
+// The same with as many workgroups as the chip holds at once, each WAVE
+// taking items of 64 consecutive blobs: its first by its number, the next
+// ones from a device-wide counter (bank epoch & 1 of two, the other zeroed
+// by workgroup 0 for the next launch on the stream).  A wave that finishes
+// early takes more, so the launch ends within about one item of its last
+// wave instead of with whole workgroups' worth of CUs idle (config 4's
+// 4096-workgroup launches lost ~12 % to that tail: scripts/sb_sizes.py).
+template <int G, bool CHACHA, int A = 2>
+__global__ __launch_bounds__(256) void k_small_q(SArgs a, uint32_t *ctr, uint32_t epoch) {
+  __shared__ uint4 lds_u4[4 * 512];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(ctr + ((epoch + 1u) & 1u) * 32u, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t *mine = ctr + (epoch & 1u) * 32u;
+  const uint64_t items = (a.n + 63) >> 6;
+  const uint32_t waves = gridDim.x * 4u;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
+  while (item < items) {  // wave-uniform
+    small_blob<G, CHACHA, A>(a, (item << 6) | lane, lds_u4);
+    uint32_t t = 0;
+    if (lane == 0)
+      t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    item = waves + uint64_t(__builtin_amdgcn_readfirstlane(t));
+  }
 }
 
 // Read side (bigblob/ref.go:113-126 getF -> cryptoXOR, blob.go:31-69): decrypt
@@ -2123,6 +2156,8 @@ struct ScratchSlot {
   uint32_t *d_err;     // the same word as the kernels address it
   DcConst *dcc;        // k_pass_dc's DcConst (device memory)
   DcConst dcc_host;    // what was last copied there
+  uint32_t *qctr;      // k_small_q: two banks of its item counter
+  uint32_t qepoch;
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
@@ -2138,7 +2173,7 @@ hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
     if (x.dev == dev && x.stream == s) sl = &x;
   if (!sl) {
     g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0, nullptr,
-                         nullptr, nullptr, nullptr, DcConst{}});
+                         nullptr, nullptr, nullptr, DcConst{}, nullptr, 0});
     sl = &g_scratch.back();
   }
   if (sl->bytes < bytes || sl->cnt_words < words) {
@@ -2357,6 +2392,64 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
 #ifndef GLFSX_SMALL_CID
 #define GLFSX_SMALL_CID 2
 #endif
+// k_small_q's counter banks on stream s (current device) and this launch's
+// epoch.
+hipError_t small_q_get(hipStream_t s, uint32_t **ctr, uint32_t *epoch) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  ScratchSlot *sl = nullptr;
+  for (ScratchSlot &x : g_scratch)
+    if (x.dev == dev && x.stream == s) sl = &x;
+  if (!sl) {
+    g_scratch.push_back({dev, s, nullptr, 0, nullptr, 0, nullptr, 0, 0, nullptr,
+                         nullptr, nullptr, nullptr, DcConst{}, nullptr, 0});
+    sl = &g_scratch.back();
+  }
+  if (!sl->qctr) {
+    e = hipMalloc(reinterpret_cast<void **>(&sl->qctr), 64 * 4);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(sl->qctr, 0, 64 * 4, s);
+    if (e != hipSuccess) return e;
+  }
+  *ctr = sl->qctr;
+  *epoch = ++sl->qepoch;
+  return hipSuccess;
+}
+
+bool small_q_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GLFSX_SMALL_Q");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Workgroups of kernel k the whole chip holds at once.
+template <class K>
+uint32_t resident_wgs(K k) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return uint32_t(std::max(per_cu, 1) * std::max(cus, 1));
+}
+
+template <int G, bool CHACHA, int A>
+hipError_t launch_small_q(const SArgs &a, hipStream_t s) {
+  static const uint32_t slots = resident_wgs(k_small_q<G, CHACHA, A>);
+  uint32_t *ctr;
+  uint32_t epoch;
+  hipError_t e = small_q_get(s, &ctr, &epoch);
+  if (e != hipSuccess) return e;
+  const uint64_t wgs = (a.n + 255) / 256;
+  const uint32_t grid = uint32_t(std::min<uint64_t>(wgs, slots ? slots : wgs));
+  hipLaunchKernelGGL((k_small_q<G, CHACHA, A>), dim3(grid), dim3(256), 0, s, a, ctr, epoch);
+  return hipGetLastError();
+}
+
 template <bool CHACHA>
 hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
@@ -2375,6 +2468,16 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   }
   // ARX form of the many-wave small-blob kernels (GLFSX_SMALL_DEK / _CID)
   constexpr int F = CHACHA ? GLFSX_SMALL_CID : GLFSX_SMALL_DEK;
+  if (small_q_enabled()) {  // more workgroups than the chip holds: per-wave items
+    switch (gsel) {
+      case 1: return launch_small_q<1, CHACHA, F>(a, s);
+      case 2: return launch_small_q<2, CHACHA, F>(a, s);
+      case 4: return launch_small_q<4, CHACHA, F>(a, s);
+      case 8: return launch_small_q<8, CHACHA, F>(a, s);
+      case 16: return launch_small_q<16, CHACHA, F>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (gsel) {
     case 1: hipLaunchKernelGGL((k_small<1, CHACHA, F>), grid, block, 0, s, a); break;
     case 2: hipLaunchKernelGGL((k_small<2, CHACHA, F>), grid, block, 0, s, a); break;
@@ -2431,6 +2534,7 @@ void release_stream_scratch(hipStream_t s) {
       if (g_scratch[i].lists) (void)hipFree(g_scratch[i].lists);
       if (g_scratch[i].err) (void)hipHostFree(g_scratch[i].err);
       if (g_scratch[i].dcc) (void)hipFree(g_scratch[i].dcc);
+      if (g_scratch[i].qctr) (void)hipFree(g_scratch[i].qctr);
     } else {
       continue;  // another device's stream of the same handle value
     }
