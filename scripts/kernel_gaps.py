@@ -1,10 +1,12 @@
 """Per-step kernel timeline from a rocprofv3 kernel trace: the kernels of one
 bigblob write (glfsx_create_device) in launch order, each with its duration
 and the idle gap before it, plus the step's GPU-busy vs first-to-last span.
-A step starts at the memset of the level-1 node buffer (the runtime's
-fillBuffer kernel) that create_device issues first.
+A step starts at each launch of the kernel named by `start` (default: the
+runtime's fillBuffer kernel if the trace has one -- round 2's per-step
+memset of the level-1 node buffer -- else the first non-fill kernel of the
+trace, e.g. k_pass_dc for config 2 or k_small_q for config 4).
 
-usage: python scripts/kernel_gaps.py <trace_dir_with_kernel_trace_csv> [skip]
+usage: python scripts/kernel_gaps.py <trace_dir_with_kernel_trace_csv> [skip] [start]
 """
 import csv
 import glob
@@ -17,15 +19,19 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-def main(d, skip=3):
+def main(d, skip=3, start=None):
     path = glob.glob(os.path.join(d, "**", "*_kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    names = [short(r["Kernel_Name"]) for r in rows]
+    if start is None:
+        start = "fillBuffer" if any("fillBuffer" in k for k in names) else \
+            next(k for k in names if not k.startswith("k_fill"))
     steps, cur = [], None
     for r in rows:
         k = short(r["Kernel_Name"])
         if k.startswith("k_fill"):
             continue
-        if "fillBuffer" in k:
+        if start in k:
             cur = []
             steps.append(cur)
         if cur is not None:
@@ -51,4 +57,5 @@ def main(d, skip=3):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3,
+         sys.argv[3] if len(sys.argv) > 3 else None)
