@@ -112,6 +112,10 @@ SIGNATURES = {
     "glfsx_tree_encode_device": (_INT, [_U64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                         _U64, _VP, ctypes.POINTER(ctypes.c_uint64), _VP]),
     "glfsx_fill_splitmix_blobs_device": (_INT, [_VP, _U64, _U64, _U64, _VP]),
+    "glfsx_post_tree_device": (_INT, [_U64, _U64, _CP, _CP, _CP, _VP, _VP, _VP, _U64, _VP,
+                                      _VP, _VP, _VP, _VP, _VP, _VP, _VP, _U64, _VP, _U64,
+                                      _VP, ctypes.POINTER(glfsx_root),
+                                      ctypes.POINTER(ctypes.c_uint64), _VP]),
     "glfsx_store_new": (_VP, [_U64, _INT, _U64, _INT, _CP]),
     "glfsx_store_free": (None, [_VP]),
     "glfsx_store_post": (_INT, [_VP, _INT, _VP, _VP, _U64]),

@@ -98,6 +98,11 @@ struct Ctx {
   PinBuf h_small, h_root;      // h_root: a root ref written by the kernels
   PinBuf h_oin, h_oct, h_oref;  // glfsx_post's one-shot staging
   PinBuf h_bin, h_bct, h_bref;  // glfsx_post_blobs' one-shot staging
+  // glfsx_post_tree_device: a second stream for the tree blob's posts, its
+  // events, and the tree layout on the host
+  hipStream_t stream2 = nullptr;
+  std::vector<hipEvent_t> events;
+  PinBuf h_tree;
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
@@ -2483,6 +2488,185 @@ int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
                          total - (n - 1) * block_size,
                          static_cast<const uint8_t *>(d_refs), pick_stream(c, stream)));
   return 0;
+}
+
+// BASELINE config 4 in one call, device-resident: tree.go:250-320's
+// PostTreeMap over n entries whose blobs are glfs.PostBlob'd (machine.go:64)
+// -- blob roots (glfsx_post_blobs_device), the tree's JSON lines
+// (glfsx_tree_encode_device) and the tree blob's Create
+// (glfsx_create_device) -- with the three overlapped: the lines' layout
+// does not depend on the roots' values (hex fields are fixed width), so it
+// is computed on a second stream while the blobs hash; the blobs are hashed
+// in `batches` groups of entry workgroups, each followed by its lines, and
+// every tree block whose bytes are all written is posted on the second
+// stream while the next group hashes.  Same bytes and roots as the three
+// calls in sequence (tests/test_gpu_tree_read.py).  Blobs above 16 KiB, a
+// tree block size that is not a multiple of 64, or no line buffer take the
+// three calls in sequence.
+namespace {
+int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
+                          const uint8_t *tree_salt, const uint8_t *cid_key,
+                          const void *d_data, const uint64_t *d_offsets,
+                          const uint64_t *d_lengths, uint64_t max_len, void *d_ctext,
+                          void *d_roots, const uint8_t *d_names,
+                          const uint64_t *d_name_offs, const uint32_t *d_modes,
+                          const uint8_t *d_types, const uint64_t *d_type_offs,
+                          const uint64_t *d_block_sizes, uint64_t tree_bs, void *d_lines,
+                          uint64_t lines_cap, void *d_tree_ctext, glfsx_root *tree_root,
+                          uint64_t *lines_len, void *stream) {
+  if (!tree_root || !lines_len) return fail(GLFSX_E_ARG, "null argument");
+  if (int e = check_block_size(blob_bs)) return e;
+  if (int e = check_block_size(tree_bs)) return e;
+  static const uint64_t batches = [] {
+    const char *e = getenv("GLFSX_TREE_BATCHES");
+    return std::max<uint64_t>(1, e ? strtoull(e, nullptr, 10) : 2);
+  }();
+  if (n == 0 || max_len > kMaxSmallLen || tree_bs % 64 || !d_lines) {
+    if (int e = glfsx_post_blobs_device(blob_bs, blob_salt, cid_key, d_data, d_offsets,
+                                        d_lengths, n, max_len, d_ctext, d_roots, stream))
+      return e;
+    if (int e = glfsx_tree_encode_device(n, d_names, d_name_offs, d_modes, d_types,
+                                         d_type_offs, static_cast<const uint8_t *>(d_roots),
+                                         d_lengths, d_block_sizes, d_lines, lines_cap,
+                                         nullptr, lines_len, stream))
+      return e;
+    return glfsx_create_device(tree_bs, tree_salt, cid_key, d_lines, *lines_len,
+                               d_tree_ctext, tree_root, nullptr, stream);
+  }
+  if (!d_data || !d_offsets || !d_lengths || !d_roots || !d_name_offs || !d_modes ||
+      !d_type_offs || !d_block_sizes)
+    return fail(GLFSX_E_ARG, "null argument");
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  hipStream_t A = pick_stream(c, stream);
+  if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  hipStream_t B = c->stream2;
+  const uint64_t wgs = (n + kTreeWG - 1) / kTreeWG;
+  const uint64_t K = std::min(batches, wgs);
+  while (c->events.size() < K + 2) {
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->events.push_back(ev);
+  }
+  Salts bsalts, tsalts;
+  if (int e = derive_salts(c, blob_salt, &bsalts)) return e;
+  if (int e = derive_salts(c, tree_salt, &tsalts)) return e;
+  const uint64_t words = n + wgs + 1;
+  if (int e = c->d_tree.ensure(8 * words)) return e;
+  if (int e = c->h_tree.ensure(8 * (wgs + 1))) return e;
+  TreeJob tj{};
+  tj.n = n;
+  tj.names = d_names;
+  tj.name_offs = d_name_offs;
+  tj.modes = d_modes;
+  tj.types = d_types;
+  tj.type_offs = d_type_offs;
+  tj.roots = static_cast<const uint8_t *>(d_roots);
+  tj.sizes = d_lengths;
+  tj.block_sizes = d_block_sizes;
+  tj.scratch = reinterpret_cast<uint64_t *>(c->d_tree.p);
+  tj.total = tj.scratch + words - 1;
+  tj.out = static_cast<uint8_t *>(d_lines);
+  tj.cap = lines_cap;
+  // the layout on B, after everything already on A
+  HIP_TRY(hipEventRecord(c->events[K], A));
+  HIP_TRY(hipStreamWaitEvent(B, c->events[K], 0));
+  HIP_TRY(launch_tree_layout(tj, B));
+  // exclusive prefix per entry workgroup, then the total (one copy)
+  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, B));
+  HIP_TRY(hipEventRecord(c->events[K + 1], B));
+  SmallJob sj{};
+  sj.src = static_cast<const uint8_t *>(d_data);
+  sj.ctext = static_cast<uint8_t *>(d_ctext);
+  sj.max_len = max_len;
+  words_from_key(sj.raw_salt, bsalts.raw);
+  words_from_key(sj.index_salt, bsalts.index);
+  if (cid_key) {
+    words_from_key(sj.cid_key, cid_key);
+    sj.cid_keyed = true;
+  } else {
+    blake3_iv_words(sj.cid_key);
+  }
+  const uint64_t *prefix = static_cast<const uint64_t *>(c->h_tree.p);
+  uint64_t total = 0, nblk = 0, t_done = 0;
+  uint8_t *lvl = nullptr;
+  for (uint64_t b = 0; b < K; ++b) {
+    const uint64_t g0 = wgs * b / K, g1 = wgs * (b + 1) / K;
+    const uint64_t e0 = g0 * kTreeWG, e1 = std::min(n, g1 * kTreeWG);
+    sj.offs = d_offsets + e0;
+    sj.lens = d_lengths + e0;
+    sj.n = e1 - e0;
+    sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e0;
+    HIP_TRY(launch_post_small(sj, A));
+    if (b == 0) {  // the layout is needed from here on (it ran beside batch 0)
+      HIP_TRY(hipEventSynchronize(c->events[K + 1]));
+      total = prefix[wgs];
+      if (total > lines_cap) {
+        HIP_TRY(hipStreamSynchronize(A));
+        *lines_len = total;
+        return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
+                    (unsigned long long)total, (unsigned long long)lines_cap);
+      }
+      nblk = (total + tree_bs - 1) / tree_bs;
+      if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
+                                tree_bs, B))
+        return e;
+      lvl = c->d_lvl_a.u8();
+    }
+    HIP_TRY(launch_tree_write(tj, g0, g1, A));
+    HIP_TRY(hipEventRecord(c->events[b], A));
+    // tree blocks whose bytes are all written now
+    const uint64_t ready = b + 1 == K ? total : prefix[g1];
+    const uint64_t t_ready = b + 1 == K ? nblk : ready / tree_bs;
+    HIP_TRY(hipStreamWaitEvent(B, c->events[b], 0));
+    if (t_ready > t_done) {
+      PostJob j{};
+      j.src = static_cast<const uint8_t *>(d_lines) + t_done * tree_bs;
+      j.ctext = d_tree_ctext ? static_cast<uint8_t *>(d_tree_ctext) + t_done * tree_bs : nullptr;
+      j.stride = tree_bs;
+      j.msg_len = tree_bs;
+      j.n = t_ready - t_done;
+      j.last_len = t_ready == nblk ? total - (nblk - 1) * tree_bs : tree_bs;
+      j.out = RefLayout{lvl + 64 * t_done, ~0ull, 0};  // ref t at byte 64t
+      words_from_key(j.salt, tsalts.raw);
+      cid_words(j, cid_key);
+      HIP_TRY(launch_post(j, B, tls_fused));
+      t_done = t_ready;
+    }
+  }
+  *lines_len = total;
+  tree_root->size = total;
+  tree_root->block_size = tree_bs;
+  if (nblk <= 1) {  // one block: its ref is the root (blob.go:190-193)
+    if (int e = c->h_root.ensure(64)) return e;
+    HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, B));
+    HIP_TRY(stream_wait(B));
+    if (int e = fused_check(B)) return e;
+    memcpy(tree_root->ref, c->h_root.p, 64);
+    return 0;
+  }
+  uint64_t posts = 0;
+  return build_up(c, B, tsalts, cid_key, tree_bs, lvl, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
+                  &c->d_lvl_b, tree_root->ref, &posts);
+}
+}  // namespace
+
+int glfsx_post_tree_device(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
+                           const uint8_t *tree_salt, const uint8_t *cid_key,
+                           const void *d_data, const uint64_t *d_offsets,
+                           const uint64_t *d_lengths, uint64_t max_len, void *d_ctext,
+                           void *d_roots, const uint8_t *d_names,
+                           const uint64_t *d_name_offs, const uint32_t *d_modes,
+                           const uint8_t *d_types, const uint64_t *d_type_offs,
+                           const uint64_t *d_block_sizes, uint64_t tree_bs, void *d_lines,
+                           uint64_t lines_cap, void *d_tree_ctext, glfsx_root *tree_root,
+                           uint64_t *lines_len, void *stream) {
+  return with_fused_retry([&] {
+    return post_tree_device_impl(n, blob_bs, blob_salt, tree_salt, cid_key, d_data, d_offsets,
+                                 d_lengths, max_len, d_ctext, d_roots, d_names, d_name_offs,
+                                 d_modes, d_types, d_type_offs, d_block_sizes, tree_bs, d_lines,
+                                 lines_cap, d_tree_ctext, tree_root, lines_len, stream);
+  });
 }
 
 int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,

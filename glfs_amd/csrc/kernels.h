@@ -151,6 +151,11 @@ struct TreeJob {
   uint64_t cap;               // bytes at out
 };
 hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
+// The same in two steps: the layout (line lengths, per-workgroup exclusive
+// prefix at scratch + n, the total) -- it does not read the roots' values --
+// and the lines of entry workgroups [wg0, wg1) (kTreeWG entries each).
+hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s);
+hipError_t launch_tree_write(const TreeJob &j, uint64_t wg0, uint64_t wg1, hipStream_t s);
 
 // n blobs of len bytes (len % 8 == 0), blob b = the splitmix stream of seed
 // seed0 + b (see oracle_fill_splitmix_blobs).

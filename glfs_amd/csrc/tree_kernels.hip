@@ -297,12 +297,15 @@ __global__ __launch_bounds__(1024) void k_tree_prefix(uint64_t *t, uint64_t m,
   if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a) {
+// wg0: the first entry workgroup of this launch (a range of them is written
+// as soon as its entries' roots exist: glfsx_post_tree_device).
+__global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a, uint32_t wg0) {
   __shared__ uint4 img4[kImg / 16];
   uint8_t *img = reinterpret_cast<uint8_t *>(img4);
-  const uint64_t i = uint64_t(blockIdx.x) * kTreeWG + threadIdx.x;
-  const uint64_t last = min<uint64_t>(uint64_t(blockIdx.x) * kTreeWG + kTreeWG - 1, a.n - 1);
-  const uint64_t base = a.wg_total[blockIdx.x];   // exclusive prefix
+  const uint64_t wg = uint64_t(blockIdx.x) + wg0;
+  const uint64_t i = wg * kTreeWG + threadIdx.x;
+  const uint64_t last = min<uint64_t>(wg * kTreeWG + kTreeWG - 1, a.n - 1);
+  const uint64_t base = a.wg_total[wg];           // exclusive prefix
   const uint64_t span = a.local_end[last];        // this workgroup's bytes
   const uint32_t sh = uint32_t((reinterpret_cast<uintptr_t>(a.out) + base) & 15);
   if (*a.total > a.cap) return;  // uniform: the caller reports the error
@@ -352,8 +355,8 @@ __global__ __launch_bounds__(256) void k_fill_blobs(uint64_t *dst, uint64_t n,
 
 }  // namespace
 
-hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
-  if (j.n == 0) return hipSuccess;
+namespace {
+TArgs tree_args(const TreeJob &j) {
   TArgs a{};
   a.n = j.n;
   a.names = j.names;
@@ -365,12 +368,37 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
   a.sizes = j.sizes;
   a.block_sizes = j.block_sizes;
   a.local_end = j.scratch;
-  const uint64_t wgs = (j.n + kTreeWG - 1) / kTreeWG;
   a.wg_total = j.scratch + j.n;
   a.line_ends = j.line_ends;
   a.out = j.out;
   a.cap = j.cap;
   a.total = j.total;
+  return a;
+}
+}  // namespace
+
+hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s) {
+  if (j.n == 0) return hipSuccess;
+  const TArgs a = tree_args(j);
+  const uint64_t wgs = (j.n + kTreeWG - 1) / kTreeWG;
+  hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs, j.total);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_write(const TreeJob &j, uint64_t wg0, uint64_t wg1, hipStream_t s) {
+  if (j.n == 0 || wg1 <= wg0 || !j.out) return hipSuccess;
+  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wg1 - wg0)), dim3(kTreeWG), 0, s,
+                     tree_args(j), uint32_t(wg0));
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
+  if (j.n == 0) return hipSuccess;
+  const TArgs a = tree_args(j);
+  const uint64_t wgs = (j.n + kTreeWG - 1) / kTreeWG;
   hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -378,7 +406,7 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
                      j.total);
   e = hipGetLastError();
   if (e != hipSuccess || !j.out) return e;
-  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
+  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a, 0u);
   return hipGetLastError();
 }
 

@@ -324,6 +324,29 @@ int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,
                              uint64_t out_cap, uint64_t *d_line_ends,
                              uint64_t *out_len, void *stream);
 
+/* BASELINE config 4 in one call (tree.go:250-320 PostTreeMap over n entries
+ * whose blobs are glfs.PostBlob'd, machine.go:64), device-resident: blob i
+ * (d_data + d_offsets[i], d_lengths[i] bytes, block size blob_bs, salt
+ * blob_salt) -> root i in d_roots (ctext to d_ctext, nullable), then entry
+ * i's JSON line (glfsx_tree_encode_device's bytes; its size field is
+ * d_lengths[i], its blockSize d_block_sizes[i]) into d_lines, then the tree
+ * blob of those lines Create'd with tree_salt at tree_bs (ctext to
+ * d_tree_ctext, nullable): *tree_root and the lines' length.  The three
+ * steps overlap (the lines' layout beside the blob hashing, tree blocks
+ * posted on a second stream as soon as their bytes are written); the
+ * results are those of glfsx_post_blobs_device, glfsx_tree_encode_device
+ * and glfsx_create_device in sequence.  Synchronises `stream`. */
+int glfsx_post_tree_device(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
+                           const uint8_t *tree_salt, const uint8_t *cid_key,
+                           const void *d_data, const uint64_t *d_offsets,
+                           const uint64_t *d_lengths, uint64_t max_len, void *d_ctext,
+                           void *d_roots, const uint8_t *d_names,
+                           const uint64_t *d_name_offs, const uint32_t *d_modes,
+                           const uint8_t *d_types, const uint64_t *d_type_offs,
+                           const uint64_t *d_block_sizes, uint64_t tree_bs, void *d_lines,
+                           uint64_t lines_cap, void *d_tree_ctext, glfsx_root *tree_root,
+                           uint64_t *lines_len, void *stream);
+
 /* --- read side (ref.go:113-126 getF decrypt) ---------- */
 /* ChaCha20, zero nonce, counter 0, key = dek (ref.go:137-144). */
 int glfsx_chacha20_xor(const uint8_t dek[32], const void *src, void *dst,

@@ -396,3 +396,106 @@ def test_config4_full_size_end_to_end(gpu, O):
     N.check(N.lib.glfsx_create_device(bs, tsalt, None, out.data_ptr(), total.value, None,
                                       ctypes.byref(r), None, None))
     assert bytes(r.ref) == want_root
+    # ------------------------------- the same in one pipelined call
+    roots2 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    out2 = torch.zeros(len(tree_bytes) + 64, dtype=torch.uint8, device="cuda")
+    r2, total2 = N.glfsx_root(), ctypes.c_uint64()
+    N.check(N.lib.glfsx_post_tree_device(n, bs, blob_salt, tsalt, None, d.data_ptr(),
+                                         offs.data_ptr(), lens.data_ptr(), ln, None,
+                                         roots2.data_ptr(), names.data_ptr(),
+                                         name_offs.data_ptr(), modes.data_ptr(),
+                                         types.data_ptr(), type_offs.data_ptr(), bss.data_ptr(),
+                                         bs, out2.data_ptr(), out2.numel(), None,
+                                         ctypes.byref(r2), ctypes.byref(total2), None))
+    torch.cuda.synchronize()
+    assert bytes(r2.ref) == want_root and r2.size == len(tree_bytes)
+    assert total2.value == len(tree_bytes)
+    assert bytes(roots2.cpu().numpy().tobytes()) == want_b
+    assert bytes(out2[:total2.value].cpu().numpy().tobytes()) == tree_bytes
+
+
+def _tree_inputs(torch, names, types, modes, sizes, bss):
+    import numpy as np
+    nb = b"".join(names)
+    tb = b"".join(types)
+    no = np.cumsum([0] + [len(x) for x in names]).astype(np.int64)
+    to = np.cumsum([0] + [len(x) for x in types]).astype(np.int64)
+    cuda = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return (cuda(np.frombuffer(nb or b"\0", dtype=np.uint8)), cuda(no),
+            cuda(np.array(modes, dtype=np.int32)), cuda(np.frombuffer(tb or b"\0", dtype=np.uint8)),
+            cuda(to), cuda(np.array(sizes, dtype=np.int64)), cuda(np.array(bss, dtype=np.int64)))
+
+
+@pytest.mark.parametrize("n,tree_bs", [(70_000, 2 * MIB), (3000, 4096), (300, 64 * 1024),
+                                       (1, 2 * MIB), (257, 1024)])
+def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
+    """glfsx_post_tree_device (blob hashing, tree lines and the tree blob
+    overlapped) against the three calls in sequence on the same inputs:
+    ragged blob sizes 0..16 KiB at odd offsets, names with JSON escapes and
+    non-ASCII bytes, every blob root, every line byte, the tree root."""
+    import ctypes
+    import random
+    import torch
+    from glfs_amd import _native as N
+    rng = random.Random(n * 7 + tree_bs)
+    lens_h = [rng.choice([0, 1, 63, 100, 1024, 4096, 5000, 16384, rng.randrange(16385)])
+              for _ in range(n)]
+    offs_h, o = [], 0
+    for ln in lens_h:
+        offs_h.append(o)
+        o += ln + rng.randrange(3)
+    data = torch.empty(o + 64, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), 0, o + 8 - o % 8, n, None))
+    names = [(b"n%06d" % i) + rng.choice([b"", b"\"", b"<&>", "é".encode(), b"\xff"])
+             for i in range(n)]
+    types = [rng.choice([b"blob", b"tree"]) for _ in range(n)]
+    modes = [rng.choice([0o644, 0o755, 0o40000]) for _ in range(n)]
+    bss = [2 * MIB] * n
+    offs = torch.tensor(offs_h, dtype=torch.int64, device="cuda")
+    lens = torch.tensor(lens_h, dtype=torch.int64, device="cuda")
+    dn, dno, dm, dt, dto, _, dbs = _tree_inputs(torch, names, types, modes, lens_h, bss)
+    bsalt, tsalt = O.derive_key(bytes(32), b"blob"), O.derive_key(bytes(32), b"tree")
+    cap = 300 * n + 4096
+    torch.cuda.synchronize()
+    # the sequence
+    roots1 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_post_blobs_device(2 * MIB, bsalt, None, data.data_ptr(),
+                                          offs.data_ptr(), lens.data_ptr(), n, 16384, None,
+                                          roots1.data_ptr(), None))
+    out1 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    t1 = ctypes.c_uint64()
+    N.check(N.lib.glfsx_tree_encode_device(n, dn.data_ptr(), dno.data_ptr(), dm.data_ptr(),
+                                           dt.data_ptr(), dto.data_ptr(), roots1.data_ptr(),
+                                           lens.data_ptr(), dbs.data_ptr(), out1.data_ptr(),
+                                           cap, None, ctypes.byref(t1), None))
+    r1 = N.glfsx_root()
+    N.check(N.lib.glfsx_create_device(tree_bs, tsalt, None, out1.data_ptr(), t1.value, None,
+                                      ctypes.byref(r1), None, None))
+    # one call
+    roots2 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    out2 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    r2, t2 = N.glfsx_root(), ctypes.c_uint64()
+    for _ in range(2):   # twice: level buffers and counters reused
+        N.check(N.lib.glfsx_post_tree_device(n, 2 * MIB, bsalt, tsalt, None, data.data_ptr(),
+                                             offs.data_ptr(), lens.data_ptr(), 16384, None,
+                                             roots2.data_ptr(), dn.data_ptr(), dno.data_ptr(),
+                                             dm.data_ptr(), dt.data_ptr(), dto.data_ptr(),
+                                             dbs.data_ptr(), tree_bs, out2.data_ptr(), cap,
+                                             None, ctypes.byref(r2), ctypes.byref(t2), None))
+        torch.cuda.synchronize()
+        assert t2.value == t1.value
+        assert bytes(r2.ref) == bytes(r1.ref)
+        assert torch.equal(roots1, roots2)
+        assert torch.equal(out1[:t1.value], out2[:t2.value])
+    # and against the oracle's Create of the lines for the tree root
+    want, _, _, _ = O.create(bytes(out1[:t1.value].cpu().numpy().tobytes()), tree_bs,
+                             salt=tsalt, closed_form=True)
+    assert bytes(r2.ref) == want
+    with pytest.raises(N.GlfsxError):   # lines above the buffer
+        N.check(N.lib.glfsx_post_tree_device(n, 2 * MIB, bsalt, tsalt, None, data.data_ptr(),
+                                             offs.data_ptr(), lens.data_ptr(), 16384, None,
+                                             roots2.data_ptr(), dn.data_ptr(), dno.data_ptr(),
+                                             dm.data_ptr(), dt.data_ptr(), dto.data_ptr(),
+                                             dbs.data_ptr(), tree_bs, out2.data_ptr(),
+                                             t1.value - 1, None, ctypes.byref(r2),
+                                             ctypes.byref(t2), None))
