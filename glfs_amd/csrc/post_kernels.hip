@@ -946,6 +946,22 @@ __device__ __forceinline__ void tree_reduce(uint32_t *lds, uint32_t k,
   }
 }
 
+// The same merge with four lanes per parent compression (quad layout, as
+// k_quad): defined after quad_compress below.  GLFSX_QTREE=0 keeps the
+// one-lane tree_reduce (A/B builds).
+#ifndef GLFSX_QTREE
+#define GLFSX_QTREE 1
+#endif
+__device__ __forceinline__ void tree_reduce_q(uint32_t *lds, uint32_t k, uint32_t t,
+                              const uint32_t (&key)[8], uint32_t base, bool root,
+                              uint32_t (&p)[8]);
+__device__ __forceinline__ void tree_merge(uint32_t *lds, uint32_t k, uint32_t t,
+                                           const uint32_t (&key)[8], uint32_t base,
+                                           bool root, uint32_t (&p)[8]) {
+  if (GLFSX_QTREE) tree_reduce_q(lds, k, t, key, base, root, p);
+  else tree_reduce(lds, k, t, key, base, root, p);
+}
+
 #if GLFSX_WGTIME
 // Phase timestamps per workgroup of the bulk passes (A/B diagnostics only,
 // tools/build_variant.sh wgtime "-DGLFSX_WGTIME=1"): [start, chunks done,
@@ -1136,7 +1152,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   }
   __syncthreads();
   WGT(bid, 1);
-  tree_reduce(lds, active, t, key, a.base, !split, cv);
+  tree_merge(lds, active, t, key, a.base, !split, cv);
   WGT(bid, 2);
   if (!split) {
     if (t == 0) {
@@ -1173,7 +1189,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
     }
   }
   __syncthreads();
-  tree_reduce(lds, W, t, key, a.base, true, cv);
+  tree_merge(lds, W, t, key, a.base, true, cv);
   if (t == 0) {
     if constexpr (FUSE == 1) publish_dek(ref + a.out_off, cv, *dc, j);
     else store_digest(ref + a.out_off, cv);
@@ -1330,6 +1346,63 @@ __device__ __forceinline__ void quad_addrs(uint32_t (&addr)[28], uint32_t slot,
                               kSched.s[r][kk[k] + 4], kSched.s[r][kk[k] + 6]);
       addr[4 * r + k] = slot + 4u * w;
     }
+  }
+}
+
+// tree_reduce with four lanes per parent: the k CVs at lds[0 .. 8k) merge
+// pairwise, parent i reading its message (CV 2i || CV 2i+1) in place as the
+// 64-B slot at lds + 16i words, 64 parents per step (256 lanes).  A one-lane
+// parent is a chain of ~700 dependent instructions; in quad layout it is
+// ~200 plus LDS reads, so the 8 levels of a 256-lane subtree (pass_body's
+// per-workgroup merge, 13-18 us in round 2's per-workgroup timeline) take
+// 9 short steps.  Same tree and flags as tree_reduce (ROOT on the last
+// parent when `root`); on return thread 0 holds the result in p.
+__device__ __forceinline__ void tree_reduce_q(uint32_t *lds, uint32_t k, uint32_t t,
+                              const uint32_t (&key)[8], uint32_t base, bool root,
+                              uint32_t (&p)[8]) {
+  const uint32_t q = t & 3u, quad = t >> 2;
+  const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
+  const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
+  const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+  uint32_t rel[28];
+  quad_addrs(rel, lds_offset(lds), q);
+  while (k > 1) {  // uniform
+    const uint32_t half = k >> 1, odd = k & 1u;
+    const uint32_t fl = base | kParent | ((root && k == 2) ? kRoot : 0u);
+    const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
+    uint32_t rl[2] = {0, 0}, rh[2] = {0, 0};
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {  // half <= 128 parents: <= 2 per quad
+      const uint32_t i = quad + 64u * r;
+      if (i < half) {  // quad-uniform
+        uint32_t addr[28];
+#pragma unroll
+        for (int x = 0; x < 28; ++x) addr[x] = rel[x] + 64u * i;
+        uint32_t cl = kq_lo, ch = kq_hi;
+        quad_compress(cl, ch, ivq, dq, addr);
+        rl[r] = cl;
+        rh[r] = ch;
+      }
+    }
+    // the odd CV moves from index k-1 to index half (its words are not
+    // among the slots being rewritten: (k-1)*8 >= half*8)
+    const uint32_t ov = (odd && t < 8) ? lds[(k - 1) * 8 + t] : 0u;
+    __syncthreads();  // every slot of this level has been read
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {
+      const uint32_t i = quad + 64u * r;
+      if (i < half) {
+        lds[i * 8 + q] = rl[r];
+        lds[i * 8 + 4 + q] = rh[r];
+      }
+    }
+    if (odd && t < 8) lds[half * 8 + t] = ov;
+    __syncthreads();
+    k = half + odd;
+  }
+  if (t == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[i] = lds[i];
   }
 }
 
@@ -1892,8 +1965,15 @@ __global__ __launch_bounds__(256) void k_small(SArgs a) {
 // early takes more, so the launch ends within about one item of its last
 // wave instead of with whole workgroups' worth of CUs idle (config 4's
 // 4096-workgroup launches lost ~12 % to that tail: scripts/sb_sizes.py).
+// GLFSX_SMALLQ_WPE waves per SIMD at least (4: at most 128 VGPRs, like
+// k_small; the loop let the CID form grow to 133 VGPRs, i.e. three waves,
+// and capping it spills 5 VGPRs: both measured)
+#ifndef GLFSX_SMALLQ_WPE
+#define GLFSX_SMALLQ_WPE 4
+#endif
 template <int G, bool CHACHA, int A = 2>
-__global__ __launch_bounds__(256) void k_small_q(SArgs a, uint32_t *ctr, uint32_t epoch) {
+__global__ __launch_bounds__(256, GLFSX_SMALLQ_WPE) void k_small_q(SArgs a, uint32_t *ctr,
+                                                                   uint32_t epoch) {
   __shared__ uint4 lds_u4[4 * 512];
   if (blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(ctr + ((epoch + 1u) & 1u) * 32u, 0u, __ATOMIC_RELAXED,
