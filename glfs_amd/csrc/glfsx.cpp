@@ -107,12 +107,21 @@ struct Ctx {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
 };
-thread_local Ctx tls_ctx;
+// One context per device the thread has used (a thread may switch devices,
+// e.g. one driving several GPUs; switching back finds its stream and
+// buffers again instead of leaking them).  Contexts live as long as the
+// thread (see ~Ctx).
+thread_local std::vector<Ctx *> tls_ctxs;
 thread_local int tls_dev = 0;
 
 int ctx_get(Ctx **out) {
-  Ctx &c = tls_ctx;
-  if (c.stream == nullptr || c.dev != tls_dev) {
+  if (tls_dev >= 0 && size_t(tls_dev) < tls_ctxs.size() && tls_ctxs[tls_dev]) {
+    Ctx &c = *tls_ctxs[tls_dev];
+    HIP_TRY(hipSetDevice(c.dev));
+    *out = &c;
+    return 0;
+  }
+  {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0)
@@ -124,14 +133,17 @@ int ctx_get(Ctx **out) {
       return fail(GLFSX_E_DEVICE, "device %d out of range (%d devices)",
                   tls_dev, n);
     HIP_TRY(hipSetDevice(tls_dev));
-    if (c.stream && c.dev != tls_dev) c = Ctx();
-    HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    c.dev = tls_dev;
-  } else {
-    HIP_TRY(hipSetDevice(c.dev));
+    auto *c = new Ctx();  // lives as long as the thread's use of the device
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return fail(GLFSX_E_DEVICE, "hipStreamCreate on device %d failed", tls_dev);
+    }
+    c->dev = tls_dev;
+    if (tls_ctxs.size() <= size_t(tls_dev)) tls_ctxs.resize(tls_dev + 1, nullptr);
+    tls_ctxs[tls_dev] = c;
+    *out = c;
+    return 0;
   }
-  *out = &c;
-  return 0;
 }
 
 // Wait for a stream whose results the caller is about to return.  Polls
