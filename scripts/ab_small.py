@@ -27,8 +27,9 @@ for r in range(reps):
             sys.exit(1)
         res[st]["small"].append(sb["small_blobs"]["value"])
         res[st]["c4"].append(c4["config4_end_to_end"]["value"])
-        print(r, st, res[st]["small"][-1], res[st]["c4"][-1],
-              c4["config4_end_to_end"].get("pieces_ms"), flush=True)
+        three = c4["config4_end_to_end"].get("three_calls", {})
+        print(r, st, "small", res[st]["small"][-1], "c4 one_call", res[st]["c4"][-1],
+              "three_calls", three.get("value"), three.get("pieces_ms"), flush=True)
 for st, d in res.items():
     print(f"[{st}] small median {statistics.median(d['small']):.2f}  "
           f"config4 median {statistics.median(d['c4']):.2f}")

@@ -14,7 +14,7 @@ sys.path.insert(0, ".")
 from glfs_amd import _native as N  # noqa: E402
 
 MIB, GIB = 1 << 20, 1 << 30
-gib = float(sys.argv[1]) if len(sys.argv) > 1 else 4.0
+gib = float(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] != "-v" else 4.0
 bs = MIB
 n = int(gib * GIB)
 host = np.empty(n, dtype=np.uint8)
@@ -30,7 +30,7 @@ root = N.glfsx_root()
 
 
 def run(lanes, sink_kind, piece, strict=False, reps=3):
-    best = None
+    best, all_ = None, []
     for _ in range(reps):
         counts = (ctypes.c_uint64 * 2)()
         st = N.lib.glfsx_store_new(bs, N.GLFSX_STORE_TRUST, 0, 0, None)
@@ -49,7 +49,10 @@ def run(lanes, sink_kind, piece, strict=False, reps=3):
         dt = time.perf_counter() - t
         N.lib.glfsx_store_free(st)
         N.check(rc)
+        all_.append(round(n / GIB / dt, 1))
         best = dt if best is None else min(best, dt)
+    if "-v" in sys.argv:
+        print("   reps", lanes, sink_kind, piece, strict, all_, flush=True)
     return round(n / GIB / best, 2)
 
 
