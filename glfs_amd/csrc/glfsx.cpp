@@ -2506,14 +2506,15 @@ int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
 // PostTreeMap over n entries whose blobs are glfs.PostBlob'd (machine.go:64)
 // -- blob roots (glfsx_post_blobs_device), the tree's JSON lines
 // (glfsx_tree_encode_device) and the tree blob's Create
-// (glfsx_create_device) -- with the three overlapped: the lines' layout
-// does not depend on the roots' values (hex fields are fixed width), so it
-// is computed on a second stream while the blobs hash; the blobs are hashed
-// in `batches` groups of entry workgroups, each followed by its lines, and
-// every tree block whose bytes are all written is posted on the second
-// stream while the next group hashes.  Same bytes and roots as the three
-// calls in sequence (tests/test_gpu_tree_read.py).  Blobs above 16 KiB, a
-// tree block size that is not a multiple of 64, or no line buffer take the
+// (glfsx_create_device) -- in one call: the lines' layout runs first (it
+// does not depend on the roots' values: hex fields are fixed width), then
+// the blobs hash and the lines are written, all queued before the host reads
+// the layout's total; the tree blob's blocks are posted on a second stream.
+// GLFSX_TREE_BATCHES > 1 hashes the entries in groups and posts each
+// group's finished tree blocks beside the next group (measured slower, see
+// `batches`).  Same bytes and roots as the three calls in sequence
+// (tests/test_gpu_tree_read.py).  Blobs above 16 KiB, a tree block size
+// that is not a multiple of 64, or no line buffer take the
 // three calls in sequence.
 namespace {
 int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
@@ -2531,7 +2532,13 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   if (int e = check_block_size(tree_bs)) return e;
   static const uint64_t batches = [] {
     const char *e = getenv("GLFSX_TREE_BATCHES");
-    return std::max<uint64_t>(1, e ? strtoull(e, nullptr, 10) : 2);
+    // 1: one hashing launch pair for all entries.  Groups of entry
+    // workgroups let the tree blob's first blocks hash beside the next
+    // group, but each group's persistent passes end in their own tail and
+    // the tree posts compete with them for the chip: config 4 one call
+    // 750 / 716 / 677 GiB/s at 1 / 2 / 4 groups (3 interleaved reps,
+    // scripts/ab_small.py, profiles/r3/ab_tree_batches.log)
+    return std::max<uint64_t>(1, e ? strtoull(e, nullptr, 10) : 1);
   }();
   if (n == 0 || max_len > kMaxSmallLen || tree_bs % 64 || !d_lines) {
     if (int e = glfsx_post_blobs_device(blob_bs, blob_salt, cid_key, d_data, d_offsets,
@@ -2580,13 +2587,17 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   tj.total = tj.scratch + words - 1;
   tj.out = static_cast<uint8_t *>(d_lines);
   tj.cap = lines_cap;
-  // the layout on B, after everything already on A
+  // B's tree posts come after everything already on A
   HIP_TRY(hipEventRecord(c->events[K], A));
   HIP_TRY(hipStreamWaitEvent(B, c->events[K], 0));
-  HIP_TRY(launch_tree_layout(tj, B));
+  // the layout first, on A: beside the hashing it is starved (the small-blob
+  // passes hold every workgroup slot of the chip, and k_tree_prefix's
+  // 1024-thread workgroup gets a CU only when a pass drains: 0.49 ms instead
+  // of 9 us, with the host blocked behind it and a 0.15 ms hole on A)
+  HIP_TRY(launch_tree_layout(tj, A));
   // exclusive prefix per entry workgroup, then the total (one copy)
-  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, B));
-  HIP_TRY(hipEventRecord(c->events[K + 1], B));
+  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, A));
+  HIP_TRY(hipEventRecord(c->events[K + 1], A));
   SmallJob sj{};
   sj.src = static_cast<const uint8_t *>(d_data);
   sj.ctext = static_cast<uint8_t *>(d_ctext);
@@ -2599,9 +2610,8 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   } else {
     blake3_iv_words(sj.cid_key);
   }
-  const uint64_t *prefix = static_cast<const uint64_t *>(c->h_tree.p);
-  uint64_t total = 0, nblk = 0, t_done = 0;
-  uint8_t *lvl = nullptr;
+  // every group's hashing and lines queued on A before the host waits for
+  // the layout (k_tree_write skips its work when the lines exceed the cap)
   for (uint64_t b = 0; b < K; ++b) {
     const uint64_t g0 = wgs * b / K, g1 = wgs * (b + 1) / K;
     const uint64_t e0 = g0 * kTreeWG, e1 = std::min(n, g1 * kTreeWG);
@@ -2610,24 +2620,27 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     sj.n = e1 - e0;
     sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e0;
     HIP_TRY(launch_post_small(sj, A));
-    if (b == 0) {  // the layout is needed from here on (it ran beside batch 0)
-      HIP_TRY(hipEventSynchronize(c->events[K + 1]));
-      total = prefix[wgs];
-      if (total > lines_cap) {
-        HIP_TRY(hipStreamSynchronize(A));
-        *lines_len = total;
-        return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
-                    (unsigned long long)total, (unsigned long long)lines_cap);
-      }
-      nblk = (total + tree_bs - 1) / tree_bs;
-      if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
-                                tree_bs, B))
-        return e;
-      lvl = c->d_lvl_a.u8();
-    }
     HIP_TRY(launch_tree_write(tj, g0, g1, A));
     HIP_TRY(hipEventRecord(c->events[b], A));
-    // tree blocks whose bytes are all written now
+  }
+  HIP_TRY(hipEventSynchronize(c->events[K + 1]));
+  const uint64_t *prefix = static_cast<const uint64_t *>(c->h_tree.p);
+  const uint64_t total = prefix[wgs];
+  if (total > lines_cap) {
+    HIP_TRY(hipStreamSynchronize(A));
+    *lines_len = total;
+    return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
+                (unsigned long long)total, (unsigned long long)lines_cap);
+  }
+  const uint64_t nblk = (total + tree_bs - 1) / tree_bs;
+  if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
+                            tree_bs, B))
+    return e;
+  uint8_t *lvl = c->d_lvl_a.u8();
+  // on B: each tree block once all its bytes are written
+  uint64_t t_done = 0;
+  for (uint64_t b = 0; b < K; ++b) {
+    const uint64_t g1 = wgs * (b + 1) / K;
     const uint64_t ready = b + 1 == K ? total : prefix[g1];
     const uint64_t t_ready = b + 1 == K ? nblk : ready / tree_bs;
     HIP_TRY(hipStreamWaitEvent(B, c->events[b], 0));
