@@ -18,9 +18,13 @@ F_OPS = ["x", "a"]      # v_xor_b32, v_add_u32
 H_OPS = ["r", "a3"]     # v_alignbit_b32, v_add3_u32
 
 
+CHAINS = [16]
+
+
 def ins(op, i):
-    r = f"%{i % 16}"
-    n = f"%{(i + 5) % 16}"
+    c = CHAINS[0]
+    r = f"%{i % c}"
+    n = f"%{(i % c + 8) % 16}" if c <= 8 else f"%{(i + 5) % 16}"
     return {
         "x": f"v_xor_b32 {r}, {r}, {n}",
         "a": f"v_add_u32 {r}, {r}, {n}",
@@ -55,8 +59,10 @@ PATTERNS = {
 }
 
 
-def body(name, ops):
-    text = "\\n".join(ins(op, i) for i, op in enumerate(ops))
+def body(name, ops, chains=16, nop=False):
+    CHAINS[0] = chains
+    sep = "\\ns_nop 0\\n" if nop else "\\n"
+    text = sep.join(ins(op, i) for i, op in enumerate(ops))
     outs = ",".join(f'"+v"(r[{i}])' for i in range(16))
     return f"""
 __device__ __forceinline__ void body_{name}(uint32_t *r, uint32_t k) {{
@@ -105,6 +111,17 @@ for n in ["b4", "b8", "b16", "b32", "qr_b16"]:
     bodies[pn] = seq(rot)
     src.append(body(pn, bodies[pn]))
     KERNELS.append((n + "_phase", n, pn))
+# dependent chains (form 1 of the headline CID pass is one chain per wave
+# with s_nop 0 between dependent instructions): QR order F F H, G order
+# H F H F F H (add3, xor, rot, add, xor, rot)
+DEP = {"qr": ["F", "F", "H"] * 21 + ["F"], "g": ["H", "F", "H", "F", "F", "H"] * 10 + ["F"] * 4}
+for pn, p in DEP.items():
+    for ch in (1, 2, 4):
+        for nop in (False, True):
+            bn = f"dep_{pn}_c{ch}{'_nop' if nop else ''}"
+            bodies[bn] = seq(p)
+            src.append(body(bn, bodies[bn], ch, nop))
+            KERNELS.append((bn, bn, bn))
 for kn, a, b in KERNELS:
     src.append(kernel(kn, a, b))
 tbl = ",\n".join(f'  {{"{kn}", (void*)k_{kn}}}' for kn, _, _ in KERNELS)
