@@ -965,7 +965,7 @@ __device__ __forceinline__ void tree_merge(uint32_t *lds, uint32_t k, uint32_t t
 #if GLFSX_WGTIME
 // Phase timestamps per workgroup of the bulk passes (A/B diagnostics only,
 // tools/build_variant.sh wgtime "-DGLFSX_WGTIME=1"): [start, chunks done,
-// subtree done, end, HW_ID, XCC_ID, 0, 0]; DEK pass at [0, 4096), CID pass
+// subtree done, end, HW_ID, XCC_ID, k_pass_dc entry, item fetched]; DEK pass at [0, 4096), CID pass
 // at [4096, 8192).  s_memrealtime: 100 MHz.
 __device__ uint64_t g_wgtime[8192][8];
 __device__ __forceinline__ void wgt(bool chacha, uint32_t bid, int slot) {
@@ -1229,6 +1229,9 @@ __global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
   // thread 0 finds the item and leaves (workgroup number within its pass,
   // kind: 0 DEK, 1 CID, 2 none) in LDS; only those two words stay live
   if (threadIdx.x == 0) {
+#if GLFSX_WGTIME
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t sl = d.sl;
     const uint32_t n = d.n;
     uint32_t *bank = d.c->lists + (d.epoch & 1u) * kLists * kListStride;
@@ -1256,6 +1259,12 @@ __global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
     }
     lds[0] = bid;
     lds[1] = kind;
+#if GLFSX_WGTIME
+    if (kind < 2 && bid + (kind ? 4096u : 0u) < 8192u) {  // kernel entry, item fetched
+      g_wgtime[bid + (kind ? 4096u : 0u)][6] = t_entry;
+      g_wgtime[bid + (kind ? 4096u : 0u)][7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
   }
   __syncthreads();
   const uint32_t bid = __builtin_amdgcn_readfirstlane(lds[0]);
