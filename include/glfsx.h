@@ -331,9 +331,9 @@ int glfsx_tree_encode_device(uint64_t n, const uint8_t *d_names,
  * i's JSON line (glfsx_tree_encode_device's bytes; its size field is
  * d_lengths[i], its blockSize d_block_sizes[i]) into d_lines, then the tree
  * blob of those lines Create'd with tree_salt at tree_bs (ctext to
- * d_tree_ctext, nullable): *tree_root and the lines' length.  The three
- * steps overlap (the lines' layout beside the blob hashing, tree blocks
- * posted on a second stream as soon as their bytes are written); the
+ * d_tree_ctext, nullable): *tree_root and the lines' length.  All launches
+ * are queued before the host reads the lines' total (the layout first, then
+ * the hashing and the lines; the tree blob's posts on a second stream); the
  * results are those of glfsx_post_blobs_device, glfsx_tree_encode_device
  * and glfsx_create_device in sequence.  Synchronises `stream`. */
 int glfsx_post_tree_device(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
