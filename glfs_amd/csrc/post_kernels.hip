@@ -1022,8 +1022,25 @@ struct DcState {
   uint32_t epoch;
   uint32_t n;
   uint32_t sl;
+  uint32_t fine_div;  // the last ceil(m / fine_div) messages of each list
+                      // run their CID pass as fine items (0: none)
   const DcConst *c;
 };
+
+// Items of work list x (kLists lists, message j on list j % kLists): all DEK
+// items of its m messages (2^sl each), then the CID items -- coarse (2^sl per
+// message) for its first m - F messages, fine (2^(sl+1) per message, half the
+// chunks per lane) for its last F.  The run-down at the end of a launch is
+// then made of items half as long.
+__host__ __device__ __forceinline__ uint32_t dc_list_msgs(uint32_t n, uint32_t x) {
+  return n > x ? (n - x + kLists - 1u) / kLists : 0u;
+}
+__host__ __device__ __forceinline__ uint32_t dc_list_fine(uint32_t m, uint32_t fine_div) {
+  return fine_div ? (m + fine_div - 1u) / fine_div : 0u;
+}
+__host__ __device__ __forceinline__ uint32_t dc_list_items(uint32_t m, uint32_t f, uint32_t sl) {
+  return (2u * m + f) << sl;
+}
 
 // The DEK pass stores message j's DEK with agent-scope atomic stores, waits
 // for them, then sets ready[j] = epoch; the CID workgroups of message j wait
@@ -1223,7 +1240,7 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
 // all 1024 first workgroups on one word (a single counter cost config 2
 // 1.7 %), and keeps a message's DEK and CID items on one XCD.
 template <int G>
-__global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
+__global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, KArgs c, DcState d) {
   __shared__ uint4 lds_u4[512 + kStageOf<true>];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds_u4);
   // thread 0 finds the item and leaves (workgroup number within its pass,
@@ -1245,22 +1262,30 @@ __global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
     uint32_t bid = 0, kind = 2;
     for (uint32_t k = 0; k < kLists; ++k) {
       const uint32_t x = (xcc + k) & (kLists - 1u);
-      const uint32_t msgs = n > x ? (n - x + kLists - 1u) / kLists : 0u;
+      const uint32_t msgs = dc_list_msgs(n, x);
       if (msgs == 0) continue;
+      const uint32_t f = G > 1 ? dc_list_fine(msgs, d.fine_div) : 0u;
       const uint32_t t = __hip_atomic_fetch_add(bank + x * kListStride, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t nd = msgs << sl;
-      if (t < 2u * nd) {
-        const uint32_t u = t < nd ? t : t - nd;  // index within the list's pass
+      const uint32_t nd = msgs << sl, nc = (msgs - f) << sl;
+      if (t < nd + nc) {  // DEK, or coarse CID: the list's message u >> sl
+        const uint32_t u = t < nd ? t : t - nd;
         bid = ((x + kLists * (u >> sl)) << sl) | (u & ((1u << sl) - 1u));
         kind = t < nd ? 0u : 1u;
+        break;
+      }
+      if (t < dc_list_items(msgs, f, sl)) {  // fine CID: 2^(sl+1) per message
+        const uint32_t u = t - nd - nc;
+        bid = ((x + kLists * (msgs - f + (u >> (sl + 1u)))) << (sl + 1u)) |
+              (u & ((2u << sl) - 1u));
+        kind = 3u;
         break;
       }
     }
     lds[0] = bid;
     lds[1] = kind;
 #if GLFSX_WGTIME
-    if (kind < 2 && bid + (kind ? 4096u : 0u) < 8192u) {  // kernel entry, item fetched
+    if (kind != 2 && bid + (kind ? 4096u : 0u) < 8192u) {  // kernel entry, item fetched
       g_wgtime[bid + (kind ? 4096u : 0u)][6] = t_entry;
       g_wgtime[bid + (kind ? 4096u : 0u)][7] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1275,10 +1300,13 @@ __global__ __launch_bounds__(256) void k_pass_dc(KArgs a, KArgs b, DcState d) {
       __hip_atomic_store(d.c->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
-  if (kind == 0)
+  if (kind == 0) {
     pass_body<G, false, true, 2, 1>(a, bid, lds_u4, &d);
-  else
+  } else if (kind == 1) {
     pass_body<G, true, true, 2, 2>(b, bid, lds_u4, &d);
+  } else {
+    if constexpr (G > 1) pass_body<G / 2, true, true, 2, 2>(c, bid, lds_u4, &d);
+  }
 }
 
 // ---- Latency mode, BLAKE3-only passes: four lanes per chaining state ----
@@ -2674,6 +2702,16 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
   return launch_pass<false>(a, maxlen, is_aligned(job), s);
 }
 
+// GLFSX_DC_FINE: the fine-item share of k_pass_dc's CID items (the last
+// ceil(m / div) messages of each work list; 0: none)
+uint32_t dc_fine_div() {
+  static const uint32_t v = [] {
+    const char *e = getenv("GLFSX_DC_FINE");
+    return e ? uint32_t(strtoul(e, nullptr, 10)) : 4u;
+  }();
+  return v;
+}
+
 // GLFSX_FUSED=0: split-mode posts as two launches (DEK pass, then CID pass)
 bool fused_enabled() {
   static const bool on = [] {
@@ -2708,24 +2746,34 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   a.out_off = 32;
   if (quad_ok(a, maxlen, true, sl) || chunks == 0) return hipSuccess;
   a.split_log2 = sl;
-  hipError_t e = scratch_get(&a, 2 * wgs, 2 * job.n, s);
+  // scratch: DEK CVs (wgs), coarse CID CVs (wgs), fine CID CVs (2 wgs)
+  hipError_t e = scratch_get(&a, 4 * wgs, 2 * job.n, s);
   if (e != hipSuccess) return e;
   DcState d{};
   e = dc_get(job.n, s, &d);
   if (e != hipSuccess) return e;
   d.n = uint32_t(job.n);
   d.sl = sl;
+  d.fine_div = (g > 1 && sl < kMaxSplitLog2) ? dc_fine_div() : 0u;
   KArgs b = a;
   for (int i = 0; i < 8; ++i) b.key[i] = job.cid_key[i];
   b.base = job.cid_keyed ? kKeyed : 0u;
   b.out_off = 0;
   b.scratch = a.scratch + wgs * 8;
   b.cnt = a.cnt + job.n;
-  const dim3 grid(uint32_t(2 * wgs)), block(256);
+  KArgs c = b;  // fine CID items: twice the workgroups per message
+  c.split_log2 = sl + 1;
+  c.scratch = b.scratch + wgs * 8;
+  uint64_t items = 0;
+  for (uint32_t x = 0; x < kLists; ++x) {
+    const uint32_t m = dc_list_msgs(d.n, x);
+    items += dc_list_items(m, dc_list_fine(m, d.fine_div), sl);
+  }
+  const dim3 grid{uint32_t(items)}, block{256};
   switch (g) {
-    case 1: hipLaunchKernelGGL(k_pass_dc<1>, grid, block, 0, s, a, b, d); break;
-    case 2: hipLaunchKernelGGL(k_pass_dc<2>, grid, block, 0, s, a, b, d); break;
-    default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, d); break;
+    case 1: hipLaunchKernelGGL(k_pass_dc<1>, grid, block, 0, s, a, b, c, d); break;
+    case 2: hipLaunchKernelGGL(k_pass_dc<2>, grid, block, 0, s, a, b, c, d); break;
+    default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, c, d); break;
   }
   *done = true;
   return hipGetLastError();
