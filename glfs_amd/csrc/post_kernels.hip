@@ -1969,8 +1969,13 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
   // blobs packed densely) has k_pass's lane layout: stage through LDS for
   // full-line loads (and ctext stores)
   const uint32_t l = threadIdx.x & 63u;
-  const uint64_t o0 = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(off >> 32))) << 32) |
-                      __builtin_amdgcn_readfirstlane(uint32_t(off));
+  // (readfirstlane returns int: widen through uint32_t, or a low word of
+  // 2^31 or more sign-extends into the high word -- every wave of blobs in
+  // the upper 2 GiB of each 4 GiB then failed the density test below and
+  // took the per-lane path)
+  const uint64_t o0 =
+      (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(off >> 32)))) << 32) |
+      uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(off)));
   const bool dense = aligned && len == uint64_t(G) << 10 &&
                      off == o0 + (uint64_t(l) * G << 10) && (!CHACHA || cmsg);
   if (__ballot(dense) == ~0ull) {  // wave-uniform
@@ -2025,7 +2030,7 @@ __global__ __launch_bounds__(256, GLFSX_SMALLQ_WPE) void k_small_q(SArgs a, uint
     uint32_t t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    item = waves + uint64_t(__builtin_amdgcn_readfirstlane(t));
+    item = waves + uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(t)));
   }
 }
 
