@@ -1938,6 +1938,8 @@ struct SArgs {
   uint32_t key0[8];   // DEK pass: indexSalt words (empty blobs); CID pass: = key
   uint32_t base;
   uint32_t out_off;
+  uint64_t n_coarse;  // k_small_q: items [0, n_coarse) are 64 blobs (one per
+                      // lane); the blobs after them go as fine items
 };
 
 // Blob i for the calling lane (nothing when i >= n); lds_u4: the
@@ -1993,6 +1995,65 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
   store_digest(ref + a.out_off, cv);
 }
 
+// A fine item of k_small_q: 64/G blobs, G lanes per blob (lane l hashes
+// chunk l % G of blob b0 + l / G), so the item takes about 1/G of a
+// one-lane-per-blob item's time.  Handed out last, they shorten the run-down
+// at the end of the launch.  Dense blobs of exactly G KiB take k_pass's
+// staged G = 1 lane layout over the wave's contiguous 64 KiB; the G chunk
+// CVs of a blob then merge through lane shuffles (log2 G parent levels, ROOT
+// on the last: the same tree as a lane's own stack).  Anything else: one
+// lane per blob on the first 64/G lanes.
+template <int G, bool CHACHA, int A>
+__device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *lds_u4) {
+  constexpr uint32_t BPI = 64u / G;
+  const uint32_t l = threadIdx.x & 63u, c = l % G;
+  const uint64_t i = b0 + l / G;
+  const bool valid = i < a.n;
+  const uint64_t off = valid ? a.offs[i] : 0, len = valid ? a.lens[i] : 0;
+  const uint8_t *msg = a.src + off;
+  uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + off : nullptr;
+  const uint64_t o0 =
+      (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(off >> 32)))) << 32) |
+      uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(off)));
+  const bool aligned = ((reinterpret_cast<uintptr_t>(msg) |
+                         reinterpret_cast<uintptr_t>(cmsg)) & 15) == 0;
+  const bool dense = valid && aligned && len == uint64_t(G) << 10 &&
+                     off == o0 + (uint64_t(l) << 10) - (uint64_t(c) << 10) &&
+                     (!CHACHA || cmsg);
+  if (__ballot(dense) != ~0ull) {
+    small_blob<G, CHACHA, A>(a, l < BPI ? b0 + l : ~0ull, lds_u4);
+    return;
+  }
+  uint8_t *ref = a.refs + i * 64;
+  uint32_t key[8], dek[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) key[w] = a.key[w];
+  if constexpr (CHACHA) {
+    const uint32_t *dp = reinterpret_cast<const uint32_t *>(ref + 32);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) dek[w] = dp[w];
+  } else {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) dek[w] = 0;
+  }
+  uint32_t cv[8];
+  lane_subtree_full<1, CHACHA, true, A>(
+      cv, a.src + o0, CHACHA ? a.ctext + o0 : nullptr, l, false, key, a.base, dek,
+      lds_offset(lds_u4 + (threadIdx.x >> 6) * 512), 64u << 10, c - l);
+#pragma unroll
+  for (uint32_t st = 1; st < uint32_t(G); st <<= 1) {
+    uint32_t m[16];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      m[w] = cv[w];
+      m[8 + w] = uint32_t(__shfl_down(int(cv[w]), st, 64));
+      cv[w] = key[w];
+    }
+    b3_compress<A>(cv, m, 0u, 0u, 64u, a.base | kParent | (2 * st == G ? kRoot : 0u));
+  }
+  if (c == 0) store_digest(ref + a.out_off, cv);
+}
+
 template <int G, bool CHACHA, int A = 2>
 __global__ __launch_bounds__(256) void k_small(SArgs a) {
   // 4 waves x 8 KiB staging image (same layout as k_pass's)
@@ -2021,12 +2082,17 @@ __global__ __launch_bounds__(256, GLFSX_SMALLQ_WPE) void k_small_q(SArgs a, uint
     __hip_atomic_store(ctr + ((epoch + 1u) & 1u) * 32u, 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   uint32_t *mine = ctr + (epoch & 1u) * 32u;
-  const uint64_t items = (a.n + 63) >> 6;
+  constexpr uint32_t BPI = G > 1 ? 64u / G : 64u;
+  const uint64_t fine0 = a.n_coarse << 6;
+  const uint64_t items = a.n_coarse + (a.n > fine0 ? (a.n - fine0 + BPI - 1) / BPI : 0);
   const uint32_t waves = gridDim.x * 4u;
   const uint32_t lane = threadIdx.x & 63u;
   uint64_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
   while (item < items) {  // wave-uniform
-    small_blob<G, CHACHA, A>(a, (item << 6) | lane, lds_u4);
+    if (G == 1 || item < a.n_coarse)
+      small_blob<G, CHACHA, A>(a, (item << 6) | lane, lds_u4);
+    else if constexpr (G > 1)
+      small_fine<G, CHACHA, A>(a, fine0 + (item - a.n_coarse) * BPI, lds_u4);
     uint32_t t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2559,14 +2625,31 @@ uint32_t resident_wgs(K k) {
   return uint32_t(std::max(per_cu, 1) * std::max(cus, 1));
 }
 
+// GLFSX_SMALL_FINE: k_small_q hands out the last 1/div of the blobs as fine
+// items (0: none).  1 M x 4 KiB blobs, 3 interleaved reps: small blobs 911 /
+// 919 / 926 GiB/s at 0 / 4 / 8, config 4 end to end 780 / 791 / 801.
+uint32_t small_fine_div() {
+  static const uint32_t v = [] {
+    const char *e = getenv("GLFSX_SMALL_FINE");
+    return e ? uint32_t(strtoul(e, nullptr, 10)) : 8u;
+  }();
+  return v;
+}
+
 template <int G, bool CHACHA, int A>
-hipError_t launch_small_q(const SArgs &a, hipStream_t s) {
+hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
   static const uint32_t slots = resident_wgs(k_small_q<G, CHACHA, A>);
   uint32_t *ctr;
   uint32_t epoch;
   hipError_t e = small_q_get(s, &ctr, &epoch);
   if (e != hipSuccess) return e;
-  const uint64_t wgs = (a.n + 255) / 256;
+  SArgs a = a0;
+  const uint32_t div = G > 1 ? small_fine_div() : 0u;
+  const uint64_t fine = div ? a.n / div : 0;
+  a.n_coarse = (a.n - fine) >> 6;  // whole coarse items; the rest goes fine
+  const uint64_t rest = a.n - (a.n_coarse << 6), bpi = G > 1 ? 64 / G : 64;
+  const uint64_t items = a.n_coarse + (rest + bpi - 1) / bpi;
+  const uint64_t wgs = (items + 3) / 4;
   const uint32_t grid = uint32_t(std::min<uint64_t>(wgs, slots ? slots : wgs));
   hipLaunchKernelGGL((k_small_q<G, CHACHA, A>), dim3(grid), dim3(256), 0, s, a, ctr, epoch);
   return hipGetLastError();
