@@ -603,13 +603,14 @@ def test_post_blobs_device_config4_sample(gpu, O):
 
 
 @pytest.mark.parametrize("bulk", [False, True])
-@pytest.mark.parametrize("ln", [1024, 2048, 4096, 16384])
+@pytest.mark.parametrize("ln", [1024, 2048, 4096, 8192, 16384])
 def test_post_blobs_dense_vs_scattered(gpu, O, latency_wgs, ln, bulk):
     """Densely packed equal blobs take the LDS-staged wave path of k_small;
     the same blobs at permuted offsets take the per-lane path.  Every root
     and every ctext byte must agree (and sampled roots with the oracle), with
     and without ctext, with a partial last wave; latency-mode launches (the
-    compiler's ARX form) and bulk ones (latency threshold 0)."""
+    compiler's ARX form) and bulk ones (latency threshold 0: k_small_q,
+    whose last blobs go as fine items of G lanes per blob, G = 2/4/8/16)."""
     torch = _torch()
     from glfs_amd import _native as N
     if bulk:
