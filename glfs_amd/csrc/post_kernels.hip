@@ -2578,7 +2578,11 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
 #define GLFSX_SMALL_DEK 2
 #endif
 #ifndef GLFSX_SMALL_CID
-#define GLFSX_SMALL_CID 2
+// form 1 (quarter-round order), as the headline's CID pass: 928.8 vs 913.3
+// GiB/s small blobs, config 4 798.1 vs 787.3 (3 interleaved reps, after the
+// wave-offset fix; round 2 measured form 2 ahead when half the waves took
+// the per-lane path)
+#define GLFSX_SMALL_CID 1
 #endif
 // k_small_q's counter banks on stream s (current device) and this launch's
 // epoch.
