@@ -51,7 +51,7 @@ IDEAL_CYCLES_PER_BLOCK = {"dek": _COMPRESS * (1 + 1 / 16),
 INSTR_PER_BYTE = {"dek": 11.60, "cid": 26.53}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -65,7 +65,40 @@ def parse():
                    help="skip roofline/cpu/host legs (profiling runs)")
     p.add_argument("--cpu-sample-mib", type=int, default=3072)
     p.add_argument("--host-rt-gib", type=float, default=4.0)
-    return p.parse_args()
+    p.add_argument("--rehearse", action="store_true",
+                   help="allow fewer visible GPUs than --gpus: parts / ranks share "
+                        "devices round-robin (a rehearsal on one box, not a measurement)")
+    return p.parse_args(argv)
+
+
+def plan_devices(gpus: int, world: int, local: int, ndev: int, rehearse: bool):
+    """Which GPUs this process drives (one part of the blob each).
+
+    * world > 1 -- launched by torch.distributed.run, one rank per GPU: rank
+      `local` drives device `local`; --gpus must equal the world size.
+    * world == 1, gpus > 1 -- ONE process drives `gpus` devices through
+      glfsx_create_devices (the shape of a Go process on the node calling the
+      C-ABI).
+    * world == 1, gpus == 1 -- the headline, device 0.
+    Fewer visible devices than needed is an error unless `rehearse` (then
+    devices are named round-robin).  Returns (mode, devices); raises
+    ValueError with the reason."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least 1")
+    if ndev < 1:
+        raise ValueError("no GPU visible (the glfsx path has no CPU fallback)")
+    if world > 1:
+        if gpus != world:
+            raise ValueError(f"--gpus {gpus} under a launcher with WORLD_SIZE {world}: "
+                             "one rank per GPU, they must match")
+        if local >= ndev and not rehearse:
+            raise ValueError(f"rank {local} needs device {local} but only {ndev} visible "
+                             "(--rehearse shares devices)")
+        return "ranks", [local % ndev]
+    if gpus > ndev and not rehearse:
+        raise ValueError(f"--gpus {gpus} but only {ndev} GPU(s) visible "
+                         "(--rehearse shares devices round-robin)")
+    return ("one_process" if gpus > 1 else "single"), [k % ndev for k in range(gpus)]
 
 
 def main():
@@ -77,8 +110,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    dev = local % max(1, ndev)   # >1 rank per GPU only when rehearsing on 1 GPU
+    ndev = torch.cuda.device_count()   # counts without initialising the GPU
+    try:
+        mode, devs = plan_devices(args.gpus, world, local, ndev, args.rehearse)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "one_process":
+        return main_one_process(args, devs)
+    dev = devs[0]
     torch.cuda.set_device(dev)
     N.set_device(dev)
     if world > 1:
@@ -212,6 +252,224 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_one_process(args, devs):
+    """N GPUs from ONE process (BASELINE config 5's shape, the way
+    a Go process on the node drives them through the C-ABI): the blob is N
+    parts of --size-gib GiB, part k resident in HBM on devs[k] (bytes = the
+    splitmix stream at offset k x part, so the blob is the N = 1 stream over
+    N x part bytes), ctext written beside it.  One step = one
+    glfsx_create_devices call: every device posts its part's data blocks and
+    level-1 nodes at once (a worker thread per device, no collective), the
+    level-1 refs are gathered on the host and the levels above posted on
+    devs[0].  ms_per_step = the call's wall time (it returns when every part
+    and the root are done); per-device GPU times from HIP events on each
+    part's stream (glfsx_create_devices_ms)."""
+    import torch
+    from glfs_amd import _native as N
+    bs = args.block_size
+    bf = bs // 64
+    span = bs * bf                              # one level-1 node: 16 GiB at 1 MiB
+    per = max(span, int(args.size_gib * GIB) // span * span)
+    nd = len(devs)
+    total = per * nd
+    bufs, cts = [], []
+    for k, d in enumerate(devs):
+        torch.cuda.set_device(d)
+        N.set_device(d)
+        t = torch.empty(per, dtype=torch.uint8, device=f"cuda:{d}")
+        c = None if args.no_ctext else torch.empty(per, dtype=torch.uint8, device=f"cuda:{d}")
+        N.check(N.lib.glfsx_fill_splitmix_device(t.data_ptr(), k * per, per, args.seed, None))
+        bufs.append(t)
+        cts.append(c)
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+    home = devs[0]
+    torch.cuda.set_device(home)
+    N.set_device(home)
+    cdevs = (ctypes.c_int * nd)(*devs)
+    ptrs = (ctypes.c_void_p * nd)(*[t.data_ptr() for t in bufs])
+    sizes = (ctypes.c_uint64 * nd)(*([per] * nd))
+    cptrs = None if args.no_ctext else (ctypes.c_void_p * nd)(*[c.data_ptr() for c in cts])
+    root, posts = N.glfsx_root(), ctypes.c_uint64()
+    msb = (ctypes.c_float * (nd + 1))()
+
+    def step():
+        N.check(N.lib.glfsx_create_devices(bs, None, None, nd, cdevs, ptrs, sizes, cptrs, None,
+                                           ctypes.byref(root), ctypes.byref(posts)))
+        k = N.lib.glfsx_create_devices_ms(msb, nd + 1)
+        return list(msb[:max(0, min(k, nd + 1))])
+
+    def sync_all():
+        for d in sorted(set(devs)):
+            torch.cuda.synchronize(d)
+
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    t0 = time.perf_counter()
+    parts = [step() for _ in range(args.steps)]
+    sync_all()
+    dt = time.perf_counter() - t0
+    ms = dt / args.steps * 1e3
+    mean = [sum(p[k] for p in parts) / len(parts) for k in range(len(parts[0]))] if parts else []
+    out = {
+        "metric": "GiB/s hashed, device-resident 1 MiB chunks, bigblob write; 1/2/4/8 MI355X",
+        "value": round(total / GIB * args.steps / dt, 2),
+        "unit": "GiB/s",
+        "n_gpus": nd,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (splitmix64 byte stream, generated in HBM on each GPU)",
+        "config": {"workload": f"bigblob write {per / GIB:g} GiB/GPU @ {bs // 1024} KiB "
+                               f"blocks, device-resident, ctext "
+                               f"{'off' if args.no_ctext else 'to HBM'}",
+                   "blob_bytes": total, "block_size": bs, "blocks": total // bs,
+                   "posts_per_step": posts.value,
+                   "parallelism": f"disjoint block ranges x{nd}, one process "
+                                  "(glfsx_create_devices)"},
+        "devices": devs,
+        "rehearsal": len(set(devs)) < nd,
+        "root_cid": bytes(root.ref)[:32].hex(),
+        "per_device_ms": {"parts": [round(x, 3) for x in mean[:nd]],
+                          "levels_above": round(mean[nd], 3) if len(mean) > nd else None,
+                          "what": "mean GPU ms per step: each part's data blocks + level-1 "
+                                  "nodes on its device, then the levels >= 2 on devs[0] (HIP "
+                                  "events on the stream that ran them)"},
+    }
+    if not args.no_extras:
+        stream = torch.cuda.Stream(device=home)
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        out["roofline"], out["valu"] = roofline(torch, N, bufs[0], cts[0], per, bs, stream, sp,
+                                                step_ms=ms, total_bytes=per)
+        out["roofline"]["device"] = home
+        del bufs, cts
+        if args.host_rt_gib > 0:
+            out["host_round_trip"] = multi_lane_host(torch, N, args, devs, bs)
+    print(json.dumps(out), flush=True)
+
+
+def multi_lane_host(torch, N, args, devs, bs):
+    """One host stream over every GPU: one Writer (pre-hashed store) with its
+    batches round-robin over the devices' lanes (glfsx_writer_set_devices),
+    fed (a) from pageable memory in 64 MiB writes and (b) from a tmpfs file
+    by the parallel pread feeder (glfsx_writer_read_fd).  PCIe-inclusive,
+    never the headline value."""
+    import numpy as np
+    nd = len(devs)
+    n = int(min(args.host_rt_gib, 4.0) * GIB) // bs * bs * nd
+    host = host_stream(torch, N, n, args.seed)
+    store_post = ctypes.cast(N.lib.glfsx_store_post, N.POST_FN)
+    root = N.glfsx_root()
+    best = {}
+    for label, lanes in (("one_gpu", devs[:1]), ("all_gpus", devs)):
+        for _ in range(3):
+            st = N.lib.glfsx_store_new(bs, N.GLFSX_STORE_TRUST, 0, 0, None)
+            err = ctypes.c_int()
+            t = time.perf_counter()
+            w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, st, ctypes.byref(err))
+            assert w, N.last_error()
+            rc = N.lib.glfsx_writer_set_devices(w, (ctypes.c_int * len(lanes))(*lanes),
+                                                len(lanes))
+            if rc == 0:
+                rc = N.lib.glfsx_writer_copy(w, host.ctypes.data, n, 64 * MIB)
+            if rc == 0:
+                rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
+            msg = (N.lib.glfsx_writer_error(w) or b"").decode()
+            N.lib.glfsx_writer_free(w)
+            dt = time.perf_counter() - t
+            N.lib.glfsx_store_free(st)
+            N.check(rc, msg)
+            best[label] = min(best.get(label, dt), dt)
+    want = bytes(root.ref)
+    res = {"value": round(n / GIB / best["all_gpus"], 2), "unit": "GiB/s",
+           "one_gpu_value": round(n / GIB / best["one_gpu"], 2), "bytes": n,
+           "root_cid": want[:32].hex(),
+           "what": f"one Writer, one pageable host stream of {n / GIB:g} GiB in 64 MiB "
+                   f"writes, batches round-robin over {nd} GPUs (glfsx_writer_set_devices), "
+                   "pre-hashed store; one_gpu_value: the same on the first GPU only; best "
+                   "of 3"}
+    res["file_feed"] = file_feed(N, host, bs, {"lanes_all": list(devs)}, want)
+    del host
+    return res
+
+
+def host_stream(torch, N, n, seed):
+    """n bytes of the splitmix stream in pageable host memory (generated on
+    the GPU, copied down)."""
+    import numpy as np
+    host = np.empty(n, dtype=np.uint8)
+    dev = torch.empty(64 * MIB, dtype=torch.uint8, device="cuda")
+    for off in range(0, n, 64 * MIB):
+        m = min(64 * MIB, n - off)
+        N.check(N.lib.glfsx_fill_splitmix_device(dev.data_ptr(), off, m, seed, None))
+        torch.cuda.synchronize()
+        host[off:off + m] = dev[:m].cpu().numpy()
+    del dev
+    return host
+
+
+def file_feed(N, host, bs, lane_sets, want_ref, reps=3):
+    """bigblob.Create fed by a file (glfs.go:53 io.Copy from an *os.File;
+    blob.go:209-217): the bytes of `host` written to a tmpfs file, then read
+    by glfsx_writer_read_fd -- several threads pread each batch straight into
+    the Writer's pinned staging while earlier batches upload, hash and
+    download -- into a pre-hashed store, for each lane set.  The root must
+    equal want_ref (the same bytes through glfsx_create).  Best of reps; the
+    file is removed afterwards."""
+    import tempfile
+    n = host.size
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    fd_w, path = tempfile.mkstemp(prefix="glfsx_feed_", dir=d)
+    res = {}
+    try:
+        with os.fdopen(fd_w, "wb") as f:
+            for off in range(0, n, 256 * MIB):
+                f.write(memoryview(host[off:off + 256 * MIB]))
+        store_post = ctypes.cast(N.lib.glfsx_store_post, N.POST_FN)
+        root, got = N.glfsx_root(), ctypes.c_uint64()
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            for label, lanes in lane_sets.items():
+                best = None
+                for _ in range(reps):
+                    st = N.lib.glfsx_store_new(bs, N.GLFSX_STORE_TRUST, 0, 0, None)
+                    err = ctypes.c_int()
+                    t = time.perf_counter()
+                    w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, st,
+                                               ctypes.byref(err))
+                    assert w, N.last_error()
+                    rc = 0
+                    if len(lanes) > 1:
+                        rc = N.lib.glfsx_writer_set_devices(
+                            w, (ctypes.c_int * len(lanes))(*lanes), len(lanes))
+                    if rc == 0:
+                        rc = N.lib.glfsx_writer_read_fd(w, fd, 0, n, ctypes.byref(got))
+                    if rc == 0:
+                        rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
+                    msg = (N.lib.glfsx_writer_error(w) or b"").decode()
+                    N.lib.glfsx_writer_free(w)
+                    dt = time.perf_counter() - t
+                    N.lib.glfsx_store_free(st)
+                    N.check(rc, msg)
+                    assert got.value == n and bytes(root.ref) == want_ref, "file feed root"
+                    best = dt if best is None else min(best, dt)
+                res[label] = round(n / GIB / best, 2)
+        finally:
+            os.close(fd)
+    finally:
+        os.unlink(path)
+    res["what"] = (f"bigblob.Create from a {n / GIB:g} GiB tmpfs file ({d}): "
+                   "glfsx_writer_read_fd, each 64 MiB batch pread by up to 16 threads straight "
+                   "into the pinned staging, pre-hashed store; root equal to glfsx_create's of "
+                   "the same bytes; best of 3")
+    return res
 
 
 def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, total_bytes=None):
@@ -611,15 +869,8 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     if n == 0:
         return None
     import torch
-    host = np.empty(n, dtype=np.uint8)
     # the same splitmix stream, generated on the GPU and copied down
-    dev = torch.empty(64 * MIB, dtype=torch.uint8, device="cuda")
-    for off in range(0, n, 64 * MIB):
-        m = min(64 * MIB, n - off)
-        N.check(N.lib.glfsx_fill_splitmix_device(dev.data_ptr(), off, m, args.seed, None))
-        torch.cuda.synchronize()
-        host[off:off + m] = dev[:m].cpu().numpy()
-    del dev
+    host = host_stream(torch, N, n, args.seed)
     root = N.glfsx_root()
 
     def run(sink, ctx, check):
@@ -664,6 +915,7 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     count_sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)   # native, no Python per block
     store_post = ctypes.cast(N.lib.glfsx_store_post, N.POST_FN)
     res = {"count_sink": run(count_sink, count_ctx, count_check)}
+    want_root = bytes(root.ref)
     res["trusting_store"] = run(store_post, store_ctx(N.GLFSX_STORE_TRUST, 0), store_check)
     res["hashing_store"] = run(store_post, store_ctx(N.GLFSX_STORE_HASH, 0), store_check)
     res["trusting_store_keeping_bytes"] = run(store_post, store_ctx(N.GLFSX_STORE_TRUST, 1),
@@ -729,6 +981,10 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     res["read_from_64m"] = read_from(64 * MIB)
     while stores:
         N.lib.glfsx_store_free(stores.pop())
+    home = int(torch.cuda.current_device())
+    ff = file_feed(N, host, bs, {"lanes_1": [home], "lanes_3": [home] * 3}, want_root)
+    res["file_read_fd"] = ff["lanes_1"]
+    res["file_read_fd_3_lanes"] = ff["lanes_3"]
     return {"value": res["trusting_store"], "unit": "GiB/s", "bytes": n,
             "what": "glfsx_create (bigblob Writer) from pageable host memory: staging copy, "
                     "H2D, kernels, D2H of every ctext + ref, each Post delivered in order to "
@@ -753,7 +1009,11 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                 "read_from_1m": "io.Copy through the Writer's ReadFrom (glfsx_writer_reserve"
                                 "/_commit): the reader copies 1 MiB per Read straight into "
                                 "the pinned staging (one thread, no second copy)",
-                "read_from_64m": "the same with 64 MiB Reads"}}
+                "read_from_64m": "the same with 64 MiB Reads",
+                "file_read_fd": ff["what"] + " (one lane)",
+                "file_read_fd_3_lanes": "the same, the Writer's batches over 3 lanes of the "
+                                        "one GPU ([0, 0, 0]: shared streams, more slots in "
+                                        "flight)"}}
 
 
 def one_process_multi_gpu(torch, N, args, world, bs, home):

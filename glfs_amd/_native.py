@@ -22,6 +22,7 @@ GLFSX_E_DEVICE = -4
 GLFSX_E_ARG = -5
 GLFSX_E_UNSUPPORTED = -6
 GLFSX_E_NOMEM = -7
+GLFSX_E_IO = -8
 GLFSX_STORE_TRUST = 0
 GLFSX_STORE_HASH = 1
 
@@ -52,6 +53,9 @@ class glfsx_root(ctypes.Structure):
 POST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                            ctypes.POINTER(ctypes.c_uint8), ctypes.c_void_p,
                            ctypes.c_uint64)
+# glfsx_read_at_fn: io.ReaderAt.ReadAt(ctx, buf, len, off) -> count / 0 / < 0
+READ_AT_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_uint64, ctypes.c_uint64)
 
 # Every entry point declared in include/glfsx.h (tests/test_abi.py checks the
 # header and the .so against this list).
@@ -79,6 +83,9 @@ SIGNATURES = {
     "glfsx_writer_reserve": (_INT, [_VP, ctypes.POINTER(ctypes.c_void_p),
                                     ctypes.POINTER(ctypes.c_uint64)]),
     "glfsx_writer_commit": (_INT, [_VP, _U64]),
+    "glfsx_writer_read_at": (_INT, [_VP, READ_AT_FN, _VP, _U64, _U64,
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+    "glfsx_writer_read_fd": (_INT, [_VP, _INT, _U64, _U64, ctypes.POINTER(ctypes.c_uint64)]),
     "glfsx_writer_write_device": (_INT, [_VP, _VP, _SZ, _VP]),
     "glfsx_writer_write_ctext": (_INT, [_VP, _VP, _U64, _U64, _VP]),
     "glfsx_writer_set_strict": (_INT, [_VP, _INT]),
@@ -94,6 +101,7 @@ SIGNATURES = {
     "glfsx_create_devices": (_INT, [_U64, _CP, _CP, _INT, _VP, _VP, _VP, _VP, _VP,
                                     ctypes.POINTER(glfsx_root),
                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "glfsx_create_devices_ms": (_INT, [ctypes.POINTER(ctypes.c_float), _INT]),
     "glfsx_shard_device": (_INT, [_U64, _CP, _CP, _VP, _U64, _U64, _U64, _VP,
                                   _VP, _VP]),
     "glfsx_root_from_level1": (_INT, [_U64, _CP, _CP, _CP, _U64, _U64,

@@ -10,6 +10,9 @@ from __future__ import annotations
 
 import ctypes
 import io
+import os
+import stat
+import time
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import BinaryIO, Optional, Protocol, Union
@@ -182,9 +185,18 @@ class Writer:
         return n
 
     def read_from(self, r) -> int:
-        """io.ReaderFrom (io.Copy in Create/Concat, blob.go:213,341, uses it):
-        r.readinto() straight into the writer's pinned staging
-        (glfsx_writer_reserve / glfsx_writer_commit), no second copy."""
+        """io.ReaderFrom (io.Copy in Create/Concat, blob.go:213,341, uses it).
+        A regular file (an *os.File, an io.ReaderAt) is read from its current
+        position to its end by several threads at once straight into the
+        writer's pinned staging (glfsx_writer_read_fd), then positioned after
+        what was read; any other stream goes r.readinto() straight into the
+        staging (glfsx_writer_reserve / glfsx_writer_commit), no second copy."""
+        fd = _regular_fd(r)
+        if fd is not None:
+            pos = r.tell()
+            got = self.read_fd(fd, pos)
+            r.seek(pos + got)
+            return got
         total = 0
         buf, cap = ctypes.c_void_p(), ctypes.c_uint64()
         while True:
@@ -192,13 +204,46 @@ class Writer:
             if rc:
                 self._raise(rc)
             view = (ctypes.c_char * cap.value).from_address(buf.value)
-            n = r.readinto(memoryview(view).cast("B")) or 0
-            rc = N.lib.glfsx_writer_commit(self._w, n)
+            n = r.readinto(memoryview(view).cast("B"))
+            rc = N.lib.glfsx_writer_commit(self._w, n or 0)
             if rc:
                 self._raise(rc)
+            if n is None:
+                # a non-blocking stream with nothing ready yet: not the end
+                # of the input (io.Copy goes on after a (0, nil) Read)
+                time.sleep(0.0005)
+                continue
             total += n
             if n == 0:
                 return total
+
+    def read_fd(self, fd: int, offset: int = 0, n: int = (1 << 64) - 1) -> int:
+        """n bytes (default: to the end) of file descriptor fd from `offset`
+        into the writer, pread by several threads at once
+        (glfsx_writer_read_fd; the descriptor's own offset is not used).
+        Returns the bytes taken."""
+        got = ctypes.c_uint64()
+        rc = N.lib.glfsx_writer_read_fd(self._w, fd, offset, n, ctypes.byref(got))
+        if rc:
+            self._raise(rc)
+        return got.value
+
+    def read_at(self, read_at, offset: int = 0, n: int = (1 << 64) - 1) -> int:
+        """io.ReaderAt route (glfsx_writer_read_at): read_at(buf: memoryview,
+        off: int) -> bytes read (0 at the end), called from several threads
+        at once on disjoint ranges.  Returns the bytes taken."""
+        def cb(_ctx, buf, ln, off):
+            try:
+                return int(read_at(memoryview((ctypes.c_char * ln).from_address(buf)).cast("B"),
+                                   off))
+            except Exception:
+                return -5   # EIO
+        fn = N.READ_AT_FN(cb)
+        got = ctypes.c_uint64()
+        rc = N.lib.glfsx_writer_read_at(self._w, fn, None, offset, n, ctypes.byref(got))
+        if rc:
+            self._raise(rc)
+        return got.value
 
     def finish(self) -> Root:
         """blob.go:135-150."""
@@ -218,6 +263,17 @@ class Writer:
             self.close()
         except Exception:
             pass
+
+
+def _regular_fd(r) -> Optional[int]:
+    """The descriptor of a seekable regular file behind r, or None."""
+    try:
+        if not (hasattr(r, "fileno") and hasattr(r, "tell") and r.seekable()):
+            return None
+        fd = r.fileno()
+        return fd if stat.S_ISREG(os.fstat(fd).st_mode) else None
+    except (OSError, ValueError, io.UnsupportedOperation):
+        return None
 
 
 def _copy(w, r: Union[bytes, bytearray, memoryview, BinaryIO]) -> None:

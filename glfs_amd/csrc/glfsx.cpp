@@ -17,7 +17,9 @@
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <cerrno>
 #include <sched.h>
+#include <unistd.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -828,16 +830,20 @@ const uint8_t *cidk(const glfsx_writer *w) {
   return w->has_cid_key ? w->cid_key : nullptr;
 }
 
-// Make `dev` current for a scope and `home` current again at its end (a
-// writer's lanes may live on other devices than its home).
+// Make `dev` current for a scope and the device that was current before it
+// current again at its end (a writer's lanes may live on other devices than
+// its home).  The device actually current is read, not assumed: scopes nest
+// (submit on lane k completes a batch of lane j, whose replay posts on the
+// home device), and a scope that trusted a `home` argument skipped the
+// switch while another lane's device was current.
 struct DevScope {
-  int home;
-  bool moved;
-  DevScope(int dev, int home_) : home(home_), moved(dev != home_) {
-    if (moved) (void)hipSetDevice(dev);
+  int prev = -1, dev;
+  explicit DevScope(int dev_) : dev(dev_) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
   }
   ~DevScope() {
-    if (moved) (void)hipSetDevice(home);
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
   }
 };
 
@@ -873,7 +879,26 @@ struct CopyTask {
   const uint8_t *src;
   size_t n;
   std::atomic<int> *left;
+  // read_at != nullptr: read n bytes at input offset `off` into dst instead
+  // (glfsx_writer_read_at); *got = bytes read, or a negative status
+  glfsx_read_at_fn read_at = nullptr;
+  void *rctx = nullptr;
+  uint64_t off = 0;
+  int64_t *got = nullptr;
 };
+
+// Read n bytes at offset off through fn, repeating short reads; stops early
+// only at the end of the input (fn returns 0) or on an error (< 0).
+int64_t read_full(glfsx_read_at_fn fn, void *ctx, uint8_t *dst, uint64_t n, uint64_t off) {
+  uint64_t done = 0;
+  while (done < n) {
+    const int64_t r = fn(ctx, dst + done, n - done, off + done);
+    if (r < 0) return r;
+    if (r == 0) break;
+    done += uint64_t(r);
+  }
+  return int64_t(done);
+}
 struct CopyPool {
   std::mutex mu;
   std::condition_variable cv;
@@ -888,7 +913,10 @@ struct CopyPool {
         t = q.back();
         q.pop_back();
       }
-      memcpy(t.dst, t.src, t.n);
+      if (t.read_at)
+        *t.got = read_full(t.read_at, t.rctx, t.dst, t.n, t.off);
+      else
+        memcpy(t.dst, t.src, t.n);
       t.left->fetch_sub(1, std::memory_order_release);
     }
   }
@@ -928,6 +956,45 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
   P.cv.notify_all();
   memcpy(dst, src, std::min(per, n));
   while (left.load(std::memory_order_acquire) > 0) sched_yield();
+}
+
+// Read n bytes of input at offset off into dst with the copy pool's threads
+// (pieces of >= 4 MiB, the caller reading the first): an io.ReaderAt / a
+// file read by several threads at once, as a page-cache copy is one core's
+// memcpy.  Returns the bytes of the contiguous prefix read (< n only at the
+// end of the input) or the first piece's error (negative).
+int64_t par_read_at(glfsx_read_at_fn fn, void *ctx, uint8_t *dst, uint64_t n, uint64_t off,
+                    unsigned max_threads) {
+  constexpr uint64_t kPiece = 4ull << 20;
+  CopyPool &P = copy_pool();
+  const uint64_t parts = std::max<uint64_t>(
+      1, std::min<uint64_t>({uint64_t(P.workers) + 1, uint64_t(max_threads), n / kPiece}));
+  if (parts <= 1) return read_full(fn, ctx, dst, n, off);
+  const uint64_t per = (n / parts + 4095) & ~uint64_t(4095);
+  std::vector<int64_t> got((n + per - 1) / per, 0);
+  std::atomic<int> left{0};
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (uint64_t o = per, k = 1; o < n; o += per, ++k) {
+      left.fetch_add(1, std::memory_order_relaxed);
+      CopyTask t{dst + o, nullptr, size_t(std::min(per, n - o)), &left};
+      t.read_at = fn;
+      t.rctx = ctx;
+      t.off = off + o;
+      t.got = &got[k];
+      P.q.push_back(t);
+    }
+  }
+  P.cv.notify_all();
+  got[0] = read_full(fn, ctx, dst, std::min(per, n), off);
+  while (left.load(std::memory_order_acquire) > 0) sched_yield();
+  uint64_t total = 0;
+  for (uint64_t k = 0; k < got.size(); ++k) {
+    if (got[k] < 0) return got[k];
+    total += uint64_t(got[k]);
+    if (uint64_t(got[k]) < std::min(per, n - k * per)) break;  // end of input
+  }
+  return int64_t(total);
 }
 
 // Post one message from host memory (ref.go:98 post + sink), synchronously,
@@ -1034,7 +1101,7 @@ int add_ref(glfsx_writer *w, size_t i, const uint8_t ref[64]) {
 // in flight is hashed again with two launches per post, in order.
 int rehash_inflight(glfsx_writer *w) {
   for (const WLane &L : w->lanes) {
-    DevScope d(L.dev, w->dev);
+    DevScope d(L.dev);
     HIP_TRY(hipStreamSynchronize(L.ws));
     HIP_TRY(hipStreamSynchronize(L.s_down));
     (void)fused_errors_take(L.ws);
@@ -1042,7 +1109,7 @@ int rehash_inflight(glfsx_writer *w) {
   for (WSlot &x : w->slot) {
     if (!x.busy) continue;
     const WLane &L = w->lanes[x.lane];
-    DevScope d(L.dev, w->dev);
+    DevScope d(L.dev);
     HIP_TRY(launch_post(x.job, L.ws, false));
     HIP_TRY(hipMemcpyAsync(x.h_refs.p, x.d_refs.p, x.nblk * 64, hipMemcpyDeviceToHost, L.ws));
     if (w->post)
@@ -1050,7 +1117,7 @@ int rehash_inflight(glfsx_writer *w) {
                              L.ws));
   }
   for (const WLane &L : w->lanes) {
-    DevScope d(L.dev, w->dev);
+    DevScope d(L.dev);
     HIP_TRY(stream_wait(L.ws));
   }
   return 0;
@@ -1064,9 +1131,13 @@ int complete(glfsx_writer *w, WSlot &sl) {
   bool failed;
   {
     const WLane &L = w->lanes[sl.lane];
-    DevScope d(L.dev, w->dev);
+    DevScope d(L.dev);
     failed = fused_errors_take(L.ws) != 0;
   }
+  // the replay's single posts (index nodes: post_one on the writer's hash
+  // stream and staging) run on the home device, whichever lane's device the
+  // caller (submit) has current
+  DevScope home(w->dev);
   if (failed)
     if (int e = rehash_inflight(w)) return e;
   sl.busy = false;
@@ -1091,7 +1162,7 @@ int submit(glfsx_writer *w) {
   const int next = (w->cur + 1) % int(w->slot.size());
   WSlot &nx = w->slot[next];
   const WLane &L = w->lanes[sl.lane];
-  DevScope dscope(L.dev, w->dev);
+  DevScope dscope(L.dev);
   const uint64_t nbytes = w->full * w->bs;
   if (int e = sl.d_in.ensure(nbytes)) return e;
   if (int e = sl.d_ct.ensure(nbytes)) return e;
@@ -1712,6 +1783,74 @@ int glfsx_writer_commit(glfsx_writer *w, uint64_t n) {
   return 0;
 }
 
+namespace {
+// Reader threads per batch of glfsx_writer_read_at (GLFSX_READ_THREADS;
+// capped by the copy pool: the GPU box's share is 16 cores).
+unsigned read_threads() {
+  static const unsigned v = [] {
+    const char *e = getenv("GLFSX_READ_THREADS");
+    return e ? std::max(1u, unsigned(strtoul(e, nullptr, 10))) : 16u;
+  }();
+  return v;
+}
+
+int64_t pread_fn(void *ctx, void *buf, uint64_t len, uint64_t off) {
+  const int fd = int(reinterpret_cast<intptr_t>(ctx));
+  for (;;) {
+    const ssize_t r = pread(fd, buf, size_t(std::min<uint64_t>(len, 1ull << 30)), off_t(off));
+    if (r >= 0) return r;
+    if (errno != EINTR) return -int64_t(errno);
+  }
+}
+}  // namespace
+
+int glfsx_writer_read_at(glfsx_writer *w, glfsx_read_at_fn read_at, void *ctx,
+                         uint64_t offset, uint64_t n, uint64_t *got) {
+  if (got) *got = 0;
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  if (!read_at) return fail(GLFSX_E_ARG, "null reader");
+  WriterCall call(w);
+  if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
+  if (w->reserved) return call.done(fail(GLFSX_E_ARG, "staging lent out by glfsx_writer_reserve"));
+  uint64_t total = 0;
+  int rc = 0;
+  while (total < n) {
+    if (int e = slot_to_host(w)) return call.done(w->sticky = e);
+    WSlot &sl = w->slot[w->cur];  // free: submit completed it before moving on
+    const uint64_t used = w->full * w->bs + w->partial;
+    const uint64_t room = w->batch_blocks * w->bs;
+    if (int e = pin_grow(sl.h_in, room, used)) return call.done(w->sticky = e);
+    const uint64_t want = std::min(room - used, n - total);
+    const int64_t r = par_read_at(read_at, ctx, sl.h_in.u8() + used, want, offset + total,
+                                  read_threads());
+    if (r < 0) {
+      rc = fail(GLFSX_E_IO, "read of %llu bytes at input offset %llu failed (%lld)",
+                (unsigned long long)want, (unsigned long long)(offset + total), (long long)r);
+      break;
+    }
+    total += uint64_t(r);
+    w->full = (used + uint64_t(r)) / w->bs;
+    w->partial = (used + uint64_t(r)) % w->bs;
+    if (w->full == w->batch_blocks)
+      if (int e = submit(w)) return call.done(w->sticky = e);
+    if (uint64_t(r) < want) break;  // the end of the input
+  }
+  if (got) *got = total;
+  if (w->strict && total)
+    if (int e = drain_strict(w)) return call.done(w->sticky = e);
+  return call.done(rc);
+}
+
+int glfsx_writer_read_fd(glfsx_writer *w, int fd, uint64_t offset, uint64_t n,
+                         uint64_t *got) {
+  if (fd < 0) {
+    if (got) *got = 0;
+    return fail(GLFSX_E_ARG, "bad file descriptor %d", fd);
+  }
+  return glfsx_writer_read_at(w, pread_fn, reinterpret_cast<void *>(intptr_t(fd)), offset, n,
+                              got);
+}
+
 int glfsx_writer_copy(glfsx_writer *w, const void *data, uint64_t n, uint64_t piece) {
   if (!w) return fail(GLFSX_E_ARG, "null writer");
   if (piece == 0) return fail(GLFSX_E_ARG, "piece of 0 bytes");
@@ -1855,7 +1994,7 @@ void glfsx_writer_free(glfsx_writer *w) {
       if (st) (void)hipStreamSynchronize(st);
     for (const WLane &L : w->lanes)
       if (L.own) {
-        DevScope d(L.dev, w->dev);
+        DevScope d(L.dev);
         for (hipStream_t st : {L.s_up, L.ws, L.s_down}) (void)hipStreamSynchronize(st);
       }
   }
@@ -1961,6 +2100,8 @@ struct PartWorker {
   bool pending = false, done = false;
   int rc = 0;
   std::string err;
+  float ms = -1.f;  // the last part's GPU time (HIP events on its stream)
+  hipEvent_t ev[2] = {nullptr, nullptr};
   void loop() {
     tls_dev = dev;
     for (;;) {
@@ -1971,12 +2112,24 @@ struct PartWorker {
         f = std::move(fn);
         pending = false;
       }
+      // the part's work runs on this thread's context stream (the calls get
+      // a null stream): events around it time the device's share of the call
+      Ctx *c = nullptr;
+      bool timed = ctx_get(&c) == 0;
+      if (timed && !ev[0])
+        timed = hipEventCreate(&ev[0]) == hipSuccess && hipEventCreate(&ev[1]) == hipSuccess;
+      if (timed) timed = hipEventRecord(ev[0], c->stream) == hipSuccess;
       const int r = f();
       std::string e = r ? tls_err : std::string();
+      float t = -1.f;
+      if (timed && hipEventRecord(ev[1], c->stream) == hipSuccess &&
+          hipEventSynchronize(ev[1]) == hipSuccess)
+        (void)hipEventElapsedTime(&t, ev[0], ev[1]);
       {
         std::lock_guard<std::mutex> lk(mu);
         rc = r;
         err = std::move(e);
+        ms = t;
         done = true;
       }
       cv.notify_all();
@@ -1989,15 +2142,19 @@ struct PartWorker {
     pending = true;
     cv.notify_all();
   }
-  int wait(std::string *e) {
+  int wait(std::string *e, float *t) {
     std::unique_lock<std::mutex> lk(mu);
     cv.wait(lk, [&] { return done; });
     *e = err;
+    *t = ms;
     return rc;
   }
 };
 std::mutex g_parts_mu;  // one glfsx_create_devices call at a time
 std::vector<std::pair<std::pair<int, int>, PartWorker *>> g_part_workers;
+// per part of the last glfsx_create_devices call: data-block pass GPU ms,
+// then the levels above (on devs[0]) as one more entry
+std::vector<float> g_parts_ms;
 
 PartWorker *part_worker(int dev, int idx) {
   for (auto &x : g_part_workers)
@@ -2023,7 +2180,9 @@ int run_parts(const int *devs, std::vector<std::function<int()>> &fns) {
   std::string msg;
   for (size_t k = 0; k < fns.size(); ++k) {
     std::string e;
-    const int rc = ws[k]->wait(&e);
+    float t = -1.f;
+    const int rc = ws[k]->wait(&e, &t);
+    g_parts_ms.push_back(t);
     if (rc && !first) {
       first = rc;
       msg = "part " + std::to_string(k) + " (device " + std::to_string(devs[k]) + "): " + e;
@@ -2032,6 +2191,13 @@ int run_parts(const int *devs, std::vector<std::function<int()>> &fns) {
   return first ? fail(first, "%s", msg.c_str()) : 0;
 }
 }  // namespace
+
+int glfsx_create_devices_ms(float *ms, int cap) {
+  std::lock_guard<std::mutex> lk(g_parts_mu);
+  const int n = int(g_parts_ms.size());
+  for (int k = 0; k < std::min(n, cap); ++k) ms[k] = g_parts_ms[k];
+  return n;
+}
 
 // Create over a blob whose bytes lie on several devices (in one
 // process): part k = bytes of blocks [first_k, first_k + nb_k) on devs[k];
@@ -2062,6 +2228,7 @@ int glfsx_create_devices(uint64_t block_size, const uint8_t *salt,
   if (nparts > 1 && part_sizes[nparts - 1] == 0)
     return fail(GLFSX_E_ARG, "the last part is empty");
   std::lock_guard<std::mutex> lk(g_parts_mu);
+  g_parts_ms.clear();
   const uint64_t n0 = (size + bs - 1) / bs;
   if (nparts == 1 || n0 <= bf) {  // one part: Create on its device
     std::vector<std::function<int()>> fns{[&] {
@@ -2285,9 +2452,12 @@ int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
   } else {
     blake3_iv_words(j.cid_key);
   }
-  // blobs of <= 16 KiB: one lane each (k_small skips the others)
+  // blobs of <= min(16 KiB, block_size): one lane each (k_small skips the
+  // others; a blob longer than its block size has several blocks)
+  const uint64_t small_max = small_max_for(block_size);
+  j.small_max = small_max;
   HIP_TRY(launch_post_small(j, s));
-  if (max_len <= kMaxSmallLen) return 0;
+  if (max_len <= small_max) return 0;
   // larger blobs (the caller said some may exceed 16 KiB): find them, then
   // one post each (<= one block: the root is post(rawSalt, blob),
   // blob.go:190-193) or a whole Create (several blocks)
@@ -2296,7 +2466,7 @@ int glfsx_post_blobs_device(uint64_t block_size, const uint8_t *salt,
   HIP_TRY(hipMemcpyAsync(lens.data(), d_lengths, 8 * n, hipMemcpyDeviceToHost, s));
   HIP_TRY(stream_wait(s));
   for (uint64_t i = 0; i < n; ++i) {
-    if (lens[i] <= kMaxSmallLen) continue;
+    if (lens[i] <= small_max) continue;
     const uint8_t *src = static_cast<const uint8_t *>(d_data) + offs[i];
     uint8_t *ct = d_ctext ? static_cast<uint8_t *>(d_ctext) + offs[i] : nullptr;
     uint8_t *ref = static_cast<uint8_t *>(d_roots) + 64 * i;
@@ -2365,8 +2535,9 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
   std::vector<uint64_t> soffs(n), slens(n), med;
   std::vector<std::vector<CapturedPost>> big(n);
   uint64_t span = 0, max_len = 0, n_small = 0;
+  const uint64_t small_max = small_max_for(bs);  // one block, <= 16 KiB
   for (uint64_t i = 0; i < n; ++i) {
-    const bool small = lengths[i] <= kMaxSmallLen;
+    const bool small = lengths[i] <= small_max;
     soffs[i] = offsets[i];
     slens[i] = small ? lengths[i] : kMaxSmallLen + 1;  // skipped by k_small
     if (small) {
@@ -2452,14 +2623,14 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
                              c->stream));
     HIP_TRY(stream_wait(c->stream));
     for (uint64_t i = 0; i < n; ++i)
-      if (lengths[i] <= kMaxSmallLen) memcpy(roots_out + 64 * i, &refs[64 * i], 64);
+      if (lengths[i] <= small_max) memcpy(roots_out + 64 * i, &refs[64 * i], 64);
   }
   if (post) {
     for (uint64_t i = 0; i < n; ++i) {
       // one PostBlob per blob, in order: a small blob's single Post (a data
       // block, or the empty index node, blob.go:187-189), or a large blob's
       // whole Post sequence
-      if (lengths[i] <= kMaxSmallLen) {
+      if (lengths[i] <= small_max) {
         int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
                       h_ct.data() + offsets[i], lengths[i]);
         if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
@@ -2540,7 +2711,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     // scripts/ab_small.py, profiles/r3/ab_tree_batches.log)
     return std::max<uint64_t>(1, e ? strtoull(e, nullptr, 10) : 1);
   }();
-  if (n == 0 || max_len > kMaxSmallLen || tree_bs % 64 || !d_lines) {
+  if (n == 0 || max_len > small_max_for(blob_bs) || tree_bs % 64 || !d_lines) {
     if (int e = glfsx_post_blobs_device(blob_bs, blob_salt, cid_key, d_data, d_offsets,
                                         d_lengths, n, max_len, d_ctext, d_roots, stream))
       return e;
@@ -2602,6 +2773,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   sj.src = static_cast<const uint8_t *>(d_data);
   sj.ctext = static_cast<uint8_t *>(d_ctext);
   sj.max_len = max_len;
+  sj.small_max = small_max_for(blob_bs);
   words_from_key(sj.raw_salt, bsalts.raw);
   words_from_key(sj.index_salt, bsalts.index);
   if (cid_key) {

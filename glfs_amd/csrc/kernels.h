@@ -78,7 +78,13 @@ struct SmallJob {
   uint8_t *refs;
   uint32_t raw_salt[8], index_salt[8], cid_key[8];
   bool cid_keyed;
+  // blobs of at most small_max bytes are hashed here: min(kMaxSmallLen,
+  // the blob block size) -- a longer blob has several blocks and an index
+  // node (blob.go:120-206), so the caller Creates it (0 = kMaxSmallLen)
+  uint64_t small_max;
 };
+// The small route's limit for blobs of block size bs.
+inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
 
 // One-shot posts (ref.go:98-161 for one message of at most kMaxOneLen bytes:

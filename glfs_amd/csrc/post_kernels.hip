@@ -1940,6 +1940,7 @@ struct SArgs {
   uint32_t out_off;
   uint64_t n_coarse;  // k_small_q: items [0, n_coarse) are 64 blobs (one per
                       // lane); the blobs after them go as fine items
+  uint64_t small_max;  // longer blobs are skipped (SmallJob::small_max)
 };
 
 // Blob i for the calling lane (nothing when i >= n); lds_u4: the
@@ -1948,7 +1949,7 @@ template <int G, bool CHACHA, int A>
 __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *lds_u4) {
   if (i >= a.n) return;
   const uint64_t off = a.offs[i], len = a.lens[i];
-  if (len > kMaxSmallLen) return;  // posted by the host's large-blob route
+  if (len > a.small_max) return;  // posted by the host's large-blob route
   const uint8_t *msg = a.src + off;
   uint8_t *cmsg = (CHACHA && a.ctext) ? a.ctext + off : nullptr;
   uint8_t *ref = a.refs + i * 64;
@@ -2017,7 +2018,7 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
       uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(off)));
   const bool aligned = ((reinterpret_cast<uintptr_t>(msg) |
                          reinterpret_cast<uintptr_t>(cmsg)) & 15) == 0;
-  const bool dense = valid && aligned && len == uint64_t(G) << 10 &&
+  const bool dense = valid && aligned && len == uint64_t(G) << 10 && len <= a.small_max &&
                      off == o0 + (uint64_t(l) << 10) - (uint64_t(c) << 10) &&
                      (!CHACHA || cmsg);
   if (__ballot(dense) != ~0ull) {
@@ -2350,11 +2351,34 @@ struct ScratchSlot {
 std::mutex g_scratch_mu;
 std::vector<ScratchSlot> g_scratch;
 
+// The device stream s belongs to (the current device for the null stream),
+// current for the scope.  The scratch slots are keyed by (device, stream)
+// and allocated on the current device; a caller driving several GPUs may
+// reach here with another device current than its stream's (a
+// multi-device Writer checked a lane's error word under the wrong device
+// and missed it), so the stream, not the thread, names the device.
+struct StreamDevice {
+  int dev = 0, prev = 0;
+  hipError_t e = hipSuccess;
+  explicit StreamDevice(hipStream_t s) {
+    e = hipGetDevice(&prev);
+    if (e != hipSuccess) return;
+    dev = prev;
+    hipDevice_t d = 0;
+    if (s && hipStreamGetDevice(s, &d) == hipSuccess) dev = d;
+    if (dev != prev) e = hipSetDevice(dev);
+  }
+  ~StreamDevice() {
+    if (dev != prev) (void)hipSetDevice(prev);
+  }
+};
+
 hipError_t scratch_get(KArgs *a, uint64_t wgs, uint64_t msgs, hipStream_t s) {
   const size_t bytes = size_t(wgs) * 32, words = size_t(msgs);
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return sd.e;
+  const int dev = sd.dev;
+  hipError_t e = hipSuccess;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   ScratchSlot *sl = nullptr;
   for (ScratchSlot &x : g_scratch)
@@ -2407,9 +2431,10 @@ std::atomic<uint64_t> g_dc_timeouts{0};
 constexpr size_t kListWords = 2 * kLists * kListStride;
 
 hipError_t dc_get(uint64_t msgs, hipStream_t s, DcState *d) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return sd.e;
+  const int dev = sd.dev;
+  hipError_t e = hipSuccess;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   ScratchSlot *sl = nullptr;
   for (ScratchSlot &x : g_scratch)
@@ -2447,8 +2472,6 @@ hipError_t dc_get(uint64_t msgs, hipStream_t s, DcState *d) {
     if (e != hipSuccess) return e;
     sl->ready_words = want;  // the epoch goes on: the new flags are zero
   }
-  // zero is never an epoch; the bank parity must alternate across the wrap
-  if (++sl->epoch == 0) sl->epoch = 2;
   DcConst want{sl->ready, sl->lists, sl->d_err,
                g_dc_wait_ticks.load(std::memory_order_relaxed),
                g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed)};
@@ -2468,9 +2491,25 @@ hipError_t dc_get(uint64_t msgs, hipStream_t s, DcState *d) {
     if (e != hipSuccess) return e;
     sl->dcc_host = want;
   }
+  // The epoch advances only here, once nothing before the launch can fail
+  // (ADVICE r3): a launch with epoch e clears the counter bank of epoch e+1,
+  // so an epoch used up without a launch would leave the bank of e+2 stale.
+  // Zero is never an epoch; the bank parity must alternate across the wrap.
+  if (++sl->epoch == 0) sl->epoch = 2;
   d->epoch = sl->epoch;
   d->c = sl->dcc;
   return hipSuccess;
+}
+
+// A k_pass_dc launch failed after dc_get: its epoch was used without the
+// launch that clears the next bank, so both banks start over at zero.
+void dc_launch_failed(hipStream_t s) {
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (ScratchSlot &x : g_scratch)
+    if (x.dev == sd.dev && x.stream == s && x.lists)
+      (void)hipMemsetAsync(x.lists, 0, kListWords * 4, s);
 }
 
 // Chunks per lane (g) and log2 workgroups per message (sl) of a launch over
@@ -2587,9 +2626,10 @@ hipError_t launch_pass(KArgs a, uint64_t maxlen, bool aligned,
 // k_small_q's counter banks on stream s (current device) and this launch's
 // epoch.
 hipError_t small_q_get(hipStream_t s, uint32_t **ctr, uint32_t *epoch) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return sd.e;
+  const int dev = sd.dev;
+  hipError_t e = hipSuccess;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   ScratchSlot *sl = nullptr;
   for (ScratchSlot &x : g_scratch)
@@ -2732,11 +2772,12 @@ uint32_t set_split_target(uint32_t wgs) { return g_split_target.exchange(wgs); }
 uint32_t set_latency_wgs(uint32_t wgs) { return g_latency_wgs.exchange(wgs); }
 
 void release_stream_scratch(hipStream_t s) {
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   for (size_t i = 0; i < g_scratch.size(); ++i) {
     if (g_scratch[i].stream != s) continue;
-    int cur = 0;
-    if (hipGetDevice(&cur) == hipSuccess && cur == g_scratch[i].dev) {
+    if (sd.dev == g_scratch[i].dev) {
       if (g_scratch[i].p) (void)hipFree(g_scratch[i].p);
       if (g_scratch[i].cnt) (void)hipFree(g_scratch[i].cnt);
       if (g_scratch[i].ready) (void)hipFree(g_scratch[i].ready);
@@ -2754,11 +2795,11 @@ void release_stream_scratch(hipStream_t s) {
 }
 
 uint32_t fused_errors_take(hipStream_t s) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  StreamDevice sd(s);
+  if (sd.e != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   for (ScratchSlot &x : g_scratch)
-    if (x.dev == dev && x.stream == s && x.err) {
+    if (x.dev == sd.dev && x.stream == s && x.err) {
       const uint32_t v = __atomic_exchange_n(x.err, 0u, __ATOMIC_ACQ_REL);
       if (v) {
         g_dc_timeouts.fetch_add(1, std::memory_order_relaxed);
@@ -2868,7 +2909,9 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
     default: hipLaunchKernelGGL(k_pass_dc<4>, grid, block, 0, s, a, b, c, d); break;
   }
   *done = true;
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) dc_launch_failed(s);
+  return e;
 }
 
 hipError_t launch_post(const PostJob &job, hipStream_t s, bool fused) {
@@ -2931,9 +2974,12 @@ hipError_t launch_fill(uint8_t *dst, uint64_t offset, uint64_t n, uint64_t seed,
 
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   if (job.n == 0) return hipSuccess;
-  // blobs above kMaxSmallLen are skipped by k_small (posted elsewhere)
-  const uint64_t max_len = std::min(job.max_len, kMaxSmallLen);
+  // blobs above small_max are skipped by k_small (posted elsewhere)
+  const uint64_t small_max = job.small_max ? std::min(job.small_max, kMaxSmallLen)
+                                           : kMaxSmallLen;
+  const uint64_t max_len = std::min(job.max_len, small_max);
   SArgs a{};
+  a.small_max = small_max;
   a.src = job.src;
   a.ctext = job.ctext;
   a.offs = job.offs;

@@ -70,7 +70,8 @@ enum {
   GLFSX_E_DEVICE = -4,           /* no HIP device / HIP runtime error */
   GLFSX_E_ARG = -5,              /* invalid argument */
   GLFSX_E_UNSUPPORTED = -6,      /* e.g. block size above the kernels' limit */
-  GLFSX_E_NOMEM = -7
+  GLFSX_E_NOMEM = -7,
+  GLFSX_E_IO = -8                /* the input's read failed (io.Copy's read error) */
 };
 
 /* bigblob/blob.go:17-21 Root{Ref, Size, BlockSize} */
@@ -197,6 +198,26 @@ int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
  * between the two; the area is the writer's again after commit. */
 int glfsx_writer_reserve(glfsx_writer *w, void **buf, uint64_t *cap);
 int glfsx_writer_commit(glfsx_writer *w, uint64_t n);
+/* io.Copy(w, r) (blob.go:213, glfs.go:53) when r is an io.ReaderAt -- an
+ * *os.File or *io.SectionReader (bigblob.Create's caller feeding a file): the
+ * input is read straight into the writer's pinned staging by several threads
+ * at once, each a >= 4 MiB piece of the batch being filled, while earlier
+ * batches upload, hash and download (one host core's page-cache copy is the
+ * limit of a single reader).  n bytes from input offset `offset` (UINT64_MAX:
+ * to the end of the input); *got = bytes taken.  The Posts, index and root
+ * are glfsx_writer_write's of the same bytes, in block order.
+ *   read_at(ctx, buf, len, off): io.ReaderAt.ReadAt -- read up to len bytes
+ *   at input offset off into buf; return the count (> 0), 0 at the end of
+ *   the input, or negative on error.  Called from several threads at once,
+ *   on disjoint ranges.
+ * A failed read returns GLFSX_E_IO with *got = the bytes taken before it
+ * (the writer stays usable, as after io.Copy's read error); glfsx_writer_read_fd
+ * is the same over pread(2) of a file descriptor (its file offset unused). */
+typedef int64_t (*glfsx_read_at_fn)(void *ctx, void *buf, uint64_t len, uint64_t off);
+int glfsx_writer_read_at(glfsx_writer *w, glfsx_read_at_fn read_at, void *ctx,
+                         uint64_t offset, uint64_t n, uint64_t *got);
+int glfsx_writer_read_fd(glfsx_writer *w, int fd, uint64_t offset, uint64_t n,
+                         uint64_t *got);
 /* io.Copy(w, r) (blob.go:213, glfs.go:53) from an in-memory reader: n bytes
  * in glfsx_writer_write calls of `piece` bytes each (io.Copy's 32 KiB
  * buffer for a reader without WriterTo), stopping at the first error. */
@@ -253,6 +274,13 @@ int glfsx_create_devices(uint64_t block_size, const uint8_t *salt,
                          const void *const *d_parts, const uint64_t *part_sizes,
                          void *const *d_ctexts, uint8_t *level1_out,
                          glfsx_root *out, uint64_t *n_posts);
+
+/* GPU time of the last glfsx_create_devices call (no reference
+ * counterpart; measurement): ms[k] = part k's data blocks and level-1 nodes
+ * on its device (HIP events on the stream that ran them), then one entry for
+ * the levels above on devs[0] (with nparts > 1).  Writes min(count, cap)
+ * entries and returns the count (-1 = not timed). */
+int glfsx_create_devices_ms(float *ms, int cap);
 
 /* Multi-GPU shard: posts blocks [first_block, first_block + nb)
  * of a blob of `size` bytes whose bytes for that range are at d_range, plus

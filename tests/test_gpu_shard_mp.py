@@ -25,14 +25,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MIB, GIB = 1 << 20, 1 << 30
 
 
-def _worker(rank, world, port, total, bs, seed, q):
+def _worker(rank, world, port, total, bs, seed, q, dev=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
     from glfs_amd import _native as N, shard
     try:
-        torch.cuda.set_device(0)
-        N.set_device(0)
+        torch.cuda.set_device(dev)
+        N.set_device(dev)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         first, nb = shard.plan(total, bs, world)[rank]
         n = min(nb * bs, total - first * bs)
@@ -48,12 +48,15 @@ def _worker(rank, world, port, total, bs, seed, q):
         q.put((rank, 0, 0, b"", None, repr(e)))
 
 
-def _run_ranks(world, total, bs, seed):
+def _run_ranks(world, total, bs, seed, per_rank_device=False):
+    """world ranks as spawned children; rank r on device r when
+    per_rank_device (distinct GPUs), else all on device 0 (rehearsal)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.randrange(2000)
-    ps = [ctx.Process(target=_worker, args=(r, world, port, total, bs, seed, q))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, total, bs, seed, q,
+                                            r if per_rank_device else 0))
           for r in range(world)]
     [p.start() for p in ps]
     out = {}
@@ -114,16 +117,45 @@ def test_sharded_write_across_processes(gpu, O, world, bs, nblocks):
         if nb:
             assert mine == _oracle_level1(O, t, bs, first, nb), rank
     if world == 2 and bs == MIB:
-        # bench.py's own N=2 path (torch.distributed.run, 2 ranks on this
-        # GPU) must print the same root for the same 32 GiB blob (seed 3)
+        # bench.py's own N=2 path (torch.distributed.run, 2 ranks; on one
+        # GPU a rehearsal) must print the same root for the same 32 GiB
+        # blob (seed 3)
+        import torch
         env = dict(os.environ)
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                "--master-port", str(31000 + random.randrange(2000)),
                os.path.join(ROOT, "bench.py"), "--gpus", "2", "--size-gib", "16",
                "--steps", "1", "--warmup", "0", "--no-extras"]
+        if torch.cuda.device_count() < 2:
+            cmd.append("--rehearse")
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
         assert p.returncode == 0, p.stderr[-3000:]
         line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
         rec = json.loads(line)
         assert rec["n_gpus"] == 2 and rec["root_cid"] == want_root[:32].hex()
+
+
+def test_bench_one_process_gpus(gpu):
+    """bench.py --gpus 2 without a launcher drives two devices from ONE
+    process (glfsx_create_devices).  With one GPU visible it must refuse
+    (exit 2) unless --rehearse, which names device 0 twice and must print
+    n_gpus 2 and the N = 1 root of the same 32 GiB (parts = the splitmix
+    stream at offsets 0 and 16 GiB, seed 3)."""
+    import torch
+    want_root, t = _whole_root(32 * GIB, MIB, 3)
+    del t
+    torch.cuda.empty_cache()
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--size-gib", "16",
+            "--steps", "1", "--warmup", "0", "--no-extras"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if torch.cuda.device_count() < 2:
+        p = subprocess.run(base, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+        assert p.returncode == 2 and "only 1 GPU" in p.stderr, (p.returncode, p.stderr[-2000:])
+        base.append("--rehearse")
+    p = subprocess.run(base, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["root_cid"] == want_root[:32].hex()
+    assert rec["config"]["blob_bytes"] == 32 * GIB
+    assert len(rec["per_device_ms"]["parts"]) == 2

@@ -1,0 +1,116 @@
+"""Batched PostBlob when the blob block size is below the small route's 16 KiB
+(ADVICE r3): a blob longer than its block size has several data blocks and an
+index node (bigblob/blob.go:120-206), so only blobs of at most
+min(16 KiB, block_size) may be hashed one lane each; the rest must be
+Created.  Every root is checked against the oracle's Create of the blob at
+that block size with the glfs blob type salt (machine.go:50-54), through the
+host batch (glfsx_post_blobs), the device batch (glfsx_post_blobs_device) and
+the one-call tree route (glfsx_post_tree_device vs the three calls).
+"""
+import ctypes
+
+import pytest
+
+from test_gpu_tree_read import _tree_inputs
+
+pytestmark = pytest.mark.gpu
+
+LENS = [0, 1, 100, 4095, 4096, 4097, 8192, 12345, 16384, 3000, 2 * 4096 + 64]
+
+
+def _want(O, salt, bs, data, offs, lens):
+    return [O.create(data[o:o + ln], bs, salt=salt, closed_form=True)[0]
+            for o, ln in zip(offs, lens)]
+
+
+def _layout():
+    offs, o = [], 0
+    for ln in LENS:
+        offs.append(o)
+        o += ln + 16
+    return offs, o
+
+
+@pytest.mark.parametrize("bs", [4096, 8192, 1024])
+def test_post_blobs_host_small_block_size(gpu, O, bs):
+    N = gpu
+    salt = O.derive_key(bytes(32), b"blob")
+    offs, total = _layout()
+    data = O.fill_splitmix(total, 9)
+    posts = []
+
+    @N.POST_FN
+    def sink(_ctx, kind, ref, ct, n):
+        posts.append((kind, ctypes.string_at(ref, 64), n, ctypes.string_at(ct, n)))
+        return 0
+
+    n = len(LENS)
+    roots = ctypes.create_string_buffer(64 * n)
+    N.check(N.lib.glfsx_post_blobs(bs, bs, salt, None, data, (ctypes.c_uint64 * n)(*offs),
+                                   (ctypes.c_uint64 * n)(*LENS), n, sink, None, roots))
+    want = _want(O, salt, bs, data, offs, LENS)
+    got = [roots.raw[64 * i:64 * i + 64] for i in range(n)]
+    assert got == want
+    # the Posts: n sequential PostBlob calls' Post sequences
+    want_posts = []
+    for o, ln in zip(offs, LENS):
+        want_posts += O.create(data[o:o + ln], bs, salt=salt)[3]
+    assert posts == want_posts
+
+
+@pytest.mark.parametrize("bs", [4096, 8192])
+def test_post_blobs_device_small_block_size(gpu, O, bs):
+    import numpy as np
+    import torch
+    N = gpu
+    salt = O.derive_key(bytes(32), b"blob")
+    offs, total = _layout()
+    data = O.fill_splitmix(total, 10)
+    d = torch.from_numpy(np.frombuffer(data + bytes(64), dtype=np.uint8).copy()).cuda()
+    n = len(LENS)
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(LENS, dtype=torch.int64, device="cuda")
+    roots = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    N.check(N.lib.glfsx_post_blobs_device(bs, salt, None, d.data_ptr(), do.data_ptr(),
+                                          dl.data_ptr(), n, 16384, None, roots.data_ptr(),
+                                          None))
+    torch.cuda.synchronize()
+    got = bytes(roots.cpu().numpy().tobytes())
+    assert [got[64 * i:64 * i + 64] for i in range(n)] == _want(O, salt, bs, data, offs, LENS)
+
+
+def test_post_tree_device_small_blob_block_size(gpu, O):
+    """blob_bs 4 KiB with blobs up to 16 KiB: the one-call route must give the
+    oracle's blob roots and the three calls' tree root."""
+    import numpy as np
+    import torch
+    N = gpu
+    bs = 4096
+    bsalt, tsalt = O.derive_key(bytes(32), b"blob"), O.derive_key(bytes(32), b"tree")
+    offs, total = _layout()
+    data = O.fill_splitmix(total, 12)
+    d = torch.from_numpy(np.frombuffer(data + bytes(64), dtype=np.uint8).copy()).cuda()
+    n = len(LENS)
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(LENS, dtype=torch.int64, device="cuda")
+    names = [b"f%03d" % i for i in range(n)]
+    dn, dno, dm, dt, dto, _, dbs = _tree_inputs(torch, names, [b"blob"] * n, [0o644] * n, LENS,
+                                                [bs] * n)
+    cap = 300 * n + 4096
+    roots = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    lines = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    r, t = N.glfsx_root(), ctypes.c_uint64()
+    torch.cuda.synchronize()
+    N.check(N.lib.glfsx_post_tree_device(n, bs, bsalt, tsalt, None, d.data_ptr(),
+                                         do.data_ptr(), dl.data_ptr(), 16384, None,
+                                         roots.data_ptr(), dn.data_ptr(), dno.data_ptr(),
+                                         dm.data_ptr(), dt.data_ptr(), dto.data_ptr(),
+                                         dbs.data_ptr(), 2 << 20, lines.data_ptr(), cap, None,
+                                         ctypes.byref(r), ctypes.byref(t), None))
+    torch.cuda.synchronize()
+    got = bytes(roots.cpu().numpy().tobytes())
+    assert [got[64 * i:64 * i + 64] for i in range(n)] == _want(O, bsalt, bs, data, offs, LENS)
+    want_tree, _, _, _ = O.create(bytes(lines[:t.value].cpu().numpy().tobytes()), 2 << 20,
+                                  salt=tsalt, closed_form=True)
+    assert bytes(r.ref) == want_tree
