@@ -29,11 +29,19 @@ package bigblob
 #include "glfsx.h"
 
 // C cannot call a Go func value: the writer's cgo.Handle travels through
-// post_ctx and goPost dispatches on it.
-extern int goPost(void *ctx, int kind, uint8_t *ref, void *ctext, uint64_t len);
+// post_ctx as an integer (converted to void * on the C side only, so Go never
+// turns a small handle value into an unsafe.Pointer -- checkptr rejects
+// that) and goPost dispatches on it.
+extern int goPost(uintptr_t ctx, int kind, uint8_t *ref, void *ctext, uint64_t len);
 static int post_tramp(void *ctx, int kind, const uint8_t *ref, const void *ctext,
                       uint64_t len) {
-	return goPost(ctx, kind, (uint8_t *)ref, (void *)ctext, len);
+	return goPost((uintptr_t)ctx, kind, (uint8_t *)ref, (void *)ctext, len);
+}
+// io.ReaderAt.ReadAt for glfsx_writer_read_at, called from the library's
+// reader threads (cgo runs the callback on an extra M).
+extern int64_t goReadAt(uintptr_t ctx, void *buf, uint64_t len, uint64_t off);
+static int64_t read_at_tramp(void *ctx, void *buf, uint64_t len, uint64_t off) {
+	return goReadAt((uintptr_t)ctx, buf, len, off);
 }
 
 // glfsx_last_error() is thread-local and a goroutine may move to another OS
@@ -44,10 +52,17 @@ static void copy_err(char *err, size_t cap) {
 	err[cap - 1] = 0;
 }
 static glfsx_writer *writer_new(uint64_t bs, uint64_t max, const uint8_t *salt,
-                                void *h, int *rc, char *err, size_t cap) {
-	glfsx_writer *w = glfsx_writer_new(bs, max, salt, NULL, post_tramp, h, rc);
+                                uintptr_t h, int *rc, char *err, size_t cap) {
+	glfsx_writer *w = glfsx_writer_new(bs, max, salt, NULL, post_tramp, (void *)h, rc);
 	if (!w) copy_err(err, cap);
 	return w;
+}
+static int writer_read_fd(glfsx_writer *w, int fd, uint64_t off, uint64_t n, uint64_t *got) {
+	return glfsx_writer_read_fd(w, fd, off, n, got);
+}
+static int writer_read_at(glfsx_writer *w, uintptr_t h, uint64_t off, uint64_t n,
+                          uint64_t *got) {
+	return glfsx_writer_read_at(w, read_at_tramp, (void *)h, off, n, got);
 }
 static int writer_devices(glfsx_writer *w, const int *devs, int n, char *err, size_t cap) {
 	int rc = glfsx_writer_set_devices(w, devs, n);
@@ -68,10 +83,12 @@ import (
 	"errors"
 	"fmt"
 	"io"
+	"math"
 	"os"
 	"runtime/cgo"
 	"strconv"
 	"strings"
+	"sync"
 	"unsafe"
 
 	"blobcache.io/blobcache/src/bcsdk"
@@ -116,7 +133,7 @@ func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte) *Writer {
 	var rc C.int
 	var cerr [512]C.char
 	gw.w = C.writer_new(C.uint64_t(ag.blockSize), C.uint64_t(s.MaxSize()), csalt,
-		unsafe.Pointer(uintptr(gw.h)), &rc, &cerr[0], C.size_t(len(cerr)))
+		C.uintptr_t(gw.h), &rc, &cerr[0], C.size_t(len(cerr)))
 	if gw.w == nil {
 		gw.h.Delete()
 		msg := C.GoString(&cerr[0])
@@ -145,8 +162,8 @@ func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte) *Writer {
 }
 
 //export goPost
-func goPost(ctx unsafe.Pointer, kind C.int, ref *C.uint8_t, ctext unsafe.Pointer, n C.uint64_t) C.int {
-	gw := cgo.Handle(uintptr(ctx)).Value().(*gpuWriter)
+func goPost(ctx C.uintptr_t, kind C.int, ref *C.uint8_t, ctext unsafe.Pointer, n C.uint64_t) C.int {
+	gw := cgo.Handle(ctx).Value().(*gpuWriter)
 	// ctext is C memory, valid only during this call; the store copies it
 	var data []byte
 	if n > 0 {
@@ -194,12 +211,59 @@ func (gw *gpuWriter) Write(data []byte) (int, error) {
 	return len(data), nil
 }
 
-// ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341): the
-// reader fills the writer's pinned staging directly (glfsx_writer_reserve /
-// glfsx_writer_commit), so every byte is copied once, by r.Read, instead of
-// into io.Copy's 32 KiB buffer and again by Write.  C memory handed to Go as
-// a slice is fine under the cgo rules; it is not used after commit.
+// ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341).
+//   - A regular *os.File: read from its current offset to its end by the
+//     library's reader threads with pread(2), straight into the writer's
+//     pinned staging, while earlier batches hash (glfsx_writer_read_fd); the
+//     file is left positioned after what was read, as io.Copy leaves it.
+//   - An io.ReaderAt that is also an io.Seeker (*io.SectionReader, ...): the
+//     same through ReadAt from several threads (glfsx_writer_read_at).
+//   - Any other reader fills the staging directly, one Read at a time
+//     (glfsx_writer_reserve / glfsx_writer_commit): every byte is copied
+//     once, by r.Read, instead of into io.Copy's 32 KiB buffer and again by
+//     Write.  C memory handed to Go as a slice is fine under the cgo rules;
+//     it is not used after commit.
 func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
+	if f, ok := r.(*os.File); ok {
+		if st, err := f.Stat(); err == nil && st.Mode().IsRegular() {
+			if pos, err := f.Seek(0, io.SeekCurrent); err == nil {
+				var got C.uint64_t
+				rc := C.writer_read_fd(gw.w, C.int(f.Fd()), C.uint64_t(pos), C.uint64_t(math.MaxUint64), &got)
+				if _, err := f.Seek(pos+int64(got), io.SeekStart); err != nil && rc == 0 {
+					return int64(got), err
+				}
+				if rc != 0 {
+					return int64(got), gw.fail(rc)
+				}
+				return int64(got), nil
+			}
+		}
+	}
+	if ra, ok := r.(interface {
+		io.ReaderAt
+		io.Seeker
+	}); ok {
+		if pos, err := ra.Seek(0, io.SeekCurrent); err == nil {
+			end, err := ra.Seek(0, io.SeekEnd)
+			if err == nil && end >= pos {
+				rd := &readerAt{r: ra}
+				h := cgo.NewHandle(rd)
+				var got C.uint64_t
+				rc := C.writer_read_at(gw.w, C.uintptr_t(h), C.uint64_t(pos), C.uint64_t(end-pos), &got)
+				h.Delete()
+				if _, err := ra.Seek(pos+int64(got), io.SeekStart); err != nil && rc == 0 {
+					return int64(got), err
+				}
+				if rc == C.GLFSX_E_IO && rd.err != nil {
+					return int64(got), rd.err // io.Copy returns the reader's error
+				}
+				if rc != 0 {
+					return int64(got), gw.fail(rc)
+				}
+				return int64(got), nil
+			}
+		}
+	}
 	var total int64
 	for {
 		var p unsafe.Pointer
@@ -219,6 +283,29 @@ func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
 			return total, err
 		}
 	}
+}
+
+// readerAt is the io.ReaderAt behind one glfsx_writer_read_at call.
+type readerAt struct {
+	r   io.ReaderAt
+	err error
+	mu  sync.Mutex
+}
+
+//export goReadAt
+func goReadAt(ctx C.uintptr_t, buf unsafe.Pointer, n C.uint64_t, off C.uint64_t) C.int64_t {
+	ra := cgo.Handle(ctx).Value().(*readerAt)
+	k, err := ra.r.ReadAt(unsafe.Slice((*byte)(buf), int(n)), int64(off))
+	if k > 0 {
+		return C.int64_t(k) // a short count with io.EOF: the next call returns 0
+	}
+	if err == nil || err == io.EOF {
+		return 0
+	}
+	ra.mu.Lock()
+	ra.err = err
+	ra.mu.Unlock()
+	return -5 // EIO: glfsx_writer_read_at returns GLFSX_E_IO
 }
 
 // Finish mirrors blob.go:135-150.
