@@ -84,13 +84,18 @@ def test_cgo_preamble_compiles(tmp_path):
     pre = "\n".join(ln for ln in m.group(1).splitlines() if not ln.startswith("#cgo"))
     c = tmp_path / "preamble.c"
     c.write_text(pre + """
-int goPost(void *ctx, int kind, uint8_t *ref, void *ctext, uint64_t len) {
+int goPost(uintptr_t ctx, int kind, uint8_t *ref, void *ctext, uint64_t len) {
   (void)ctx; (void)kind; (void)ref; (void)ctext; (void)len; return 0;
 }
+int64_t goReadAt(uintptr_t ctx, void *buf, uint64_t len, uint64_t off) {
+  (void)ctx; (void)buf; (void)len; (void)off; return 0;
+}
 void *touch(void) {
-  static void *fns[4];
+  static void *fns[7];
   fns[0] = (void *)writer_new; fns[1] = (void *)writer_devices;
   fns[2] = (void *)derive_key; fns[3] = (void *)post_tramp;
+  fns[4] = (void *)writer_read_fd; fns[5] = (void *)writer_read_at;
+  fns[6] = (void *)read_at_tramp;
   return fns;
 }
 """)
@@ -107,5 +112,71 @@ def test_integration_md_embeds_the_shipped_files():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    assert text.count("<!-- embed: integration/go/") == 3
+    assert text.count("<!-- embed: integration/go/") == 6
     assert mod.render(text) == text, "run scripts/embed_integration.py"
+
+
+@pytest.mark.skipif(not shutil.which("gcc"), reason="no gcc")
+def test_glfs_cgo_preamble_compiles(tmp_path):
+    """glfs_gpu.go's preamble (PostBlobs / PostTreeMapGPU) compiles with gcc
+    -Werror against glfsx.h (goPostBlobs stubbed)."""
+    src = _read("glfs_gpu.go")
+    m = re.search(r"/\*\n(.*?)\*/\nimport \"C\"", src, re.S)
+    assert m, "no cgo preamble"
+    pre = "\n".join(ln for ln in m.group(1).splitlines() if not ln.startswith("#cgo"))
+    c = tmp_path / "glfs_preamble.c"
+    c.write_text(pre + """
+int goPostBlobs(uintptr_t ctx, int kind, uint8_t *ref, void *ctext, uint64_t len) {
+  (void)ctx; (void)kind; (void)ref; (void)ctext; (void)len; return 0;
+}
+void *touch(void) {
+  static void *fns[2];
+  fns[0] = (void *)post_blobs; fns[1] = (void *)tree_encode;
+  return fns;
+}
+""")
+    p = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-c",
+                        "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                        str(tmp_path / "glfs_preamble.o")], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
+def test_cgo_handles_never_become_go_pointers():
+    """a cgo.Handle (small integers from 1) converted to
+    unsafe.Pointer in Go trips checkptr; it must travel as C.uintptr_t and
+    the exported callbacks must take uintptr_t."""
+    for name in ("gpu.go", "glfs_gpu.go"):
+        src = _read(name)
+        assert not re.search(r"unsafe\.Pointer\(uintptr\(", src), name
+        for fn in re.findall(r"//export (\w+)\nfunc \w+\(([^)]*)\)", src):
+            assert fn[1].startswith("ctx C.uintptr_t"), (name, fn)
+        for ext in re.findall(r"extern \w+ (go\w+)\(([^)]*)\)", src):
+            assert ext[1].startswith("uintptr_t ctx"), (name, ext)
+
+
+def test_glfs_batch_entry_points_in_both_builds():
+    """PostBlobs / PostTreeMapGPU exist with and without the glfsgpu tag,
+    with the same signatures, in package glfs; the shared helper has no
+    build tag; the reference names they call exist in the reference."""
+    sig_pb = r"func \(ag \*Machine\) PostBlobs\(ctx context\.Context, s schema\.WO, " \
+             r"blobs \[\]\[\]byte\) \(\[\]Ref, error\)"
+    sig_tm = r"func \(ag \*Machine\) PostTreeMapGPU\(ctx context\.Context, s schema\.WO, " \
+             r"m map\[string\]Ref\) \(\*Ref, error\)"
+    for name, tag in (("glfs_gpu.go", "//go:build glfsgpu"),
+                      ("glfs_gpu_stub.go", "//go:build !glfsgpu")):
+        src = _read(name)
+        assert src.startswith(tag + "\n"), name
+        assert re.search(r"^package glfs$", src, re.M), name
+        assert re.search(sig_pb, src) and re.search(sig_tm, src), name
+        assert src.count("{") == src.count("}") and src.count("(") == src.count(")"), name
+    shared = _read("glfs_batch.go")
+    assert "//go:build" not in shared and re.search(r"^package glfs$", shared, re.M)
+    assert "func postBlobsSeq(" in shared
+    if os.path.isdir(REF):
+        ref = "".join(open(os.path.join(REF, f)).read()
+                      for f in ("machine.go", "tree.go", "glfs.go", "blob.go"))
+        for name in ("func (ag *Machine) PostTreeMap(", "func (ag *Machine) PostBlob(",
+                     "func (ag *Machine) PostTyped(", "func (ag *Machine) makeSalt(",
+                     "func SortTreeEntries(", "func CleanPath(", "func getFileMode(",
+                     "TypeBlob = ", "TypeTree = "):
+            assert name in ref, name
