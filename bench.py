@@ -247,6 +247,7 @@ def main():
             if args.host_rt_gib > 0:
                 out["config2"] = config2_leg(torch, N, stream, sp)
                 out["small_blobs"] = small_blobs(torch, N, stream, sp)
+                out["small_blobs_from_host"] = small_blobs_from_host(torch, N, stream, sp)
                 out["config4_end_to_end"] = config4_end_to_end(torch, N, stream, sp)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -662,6 +663,64 @@ def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
             "reps": reps, "stat": "mean of the reps (HIP events on the launch stream)",
             "what": "1,048,576 distinct 4 KiB blobs, glfs.PostBlob roots (DEK + ChaCha20 "
                     "ctext to HBM + CID), one lane per blob"}
+
+
+def small_blobs_from_host(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
+    """Config 4's hashing as a Go caller sees it (glfs.PostBlobs over
+    glfsx_post_blobs): 1,048,576 distinct 4 KiB blobs
+    (blob i = the splitmix stream of seed i) in pageable HOST memory, one
+    glfsx_post_blobs call -- packed into pinned 64 MiB groups, uploaded,
+    hashed one lane per blob, roots and ctext downloaded, every blob's Post
+    delivered in order to a native sink -- PCIe inside the time.  The roots
+    must equal the device-resident batch's."""
+    import numpy as np
+    from glfs_amd import glfs
+    bs = 2 << 20
+    salt = glfs.Machine().make_salt("blob")
+    with torch.cuda.stream(stream):
+        d = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
+        roots_d = torch.empty(64 * n, dtype=torch.uint8, device="cuda")
+        offs_d = torch.arange(n, dtype=torch.int64, device="cuda") * ln
+        lens_d = torch.full((n,), ln, dtype=torch.int64, device="cuda")
+        N.check(N.lib.glfsx_fill_splitmix_blobs_device(d.data_ptr(), n, ln, 0, sp))
+        N.check(N.lib.glfsx_post_blobs_device(bs, salt, None, d.data_ptr(), offs_d.data_ptr(),
+                                              lens_d.data_ptr(), n, ln, None, roots_d.data_ptr(),
+                                              sp))
+    stream.synchronize()
+    host = d.cpu().numpy()
+    want = roots_d.cpu().numpy().tobytes()
+    del d, roots_d, offs_d, lens_d
+    offs = np.arange(n, dtype=np.uint64) * ln
+    lens = np.full(n, ln, dtype=np.uint64)
+    roots = np.empty(64 * n, dtype=np.uint8)
+    counts = (ctypes.c_uint64 * 2)()
+    sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
+    res = {}
+    for label, post in (("with_posts", sink), ("roots_only", N.POST_FN(0))):
+        ts = []
+        for _ in range(reps + 1):
+            counts[0] = counts[1] = 0
+            roots[:] = 0
+            t = time.perf_counter()
+            N.check(N.lib.glfsx_post_blobs(bs, bs, salt, None, host.ctypes.data, offs.ctypes.data,
+                                           lens.ctypes.data, n, post, ctypes.byref(counts),
+                                           roots.ctypes.data))
+            ts.append(time.perf_counter() - t)
+            assert roots.tobytes() == want, "host batch roots differ from the device batch"
+            if label == "with_posts":
+                assert counts[0] == n and counts[1] == n * ln, "sink missed Posts"
+        sec = sum(ts[1:]) / reps
+        res[label] = {"value": round(n * ln / GIB / sec, 2), "ms": round(sec * 1e3, 2),
+                      "blobs_per_s": round(n / sec)}
+    out = dict(res["with_posts"])
+    out.update({"unit": "GiB/s", "reps": reps, "stat": "mean wall time after one warm-up call",
+                "roots_only": res["roots_only"],
+                "what": "1,048,576 x 4 KiB glfs blobs from pageable host memory through one "
+                        "glfsx_post_blobs call (glfs.PostBlobs): pinned 64 MiB groups, H2D, "
+                        "one lane per blob, roots + ctext D2H, every Post delivered in order "
+                        "(native counting sink); roots_only: no sink, so no ctext download. "
+                        "Roots equal the device batch's"})
+    return out
 
 
 def config2_leg(torch, N, stream, sp, steps=50, warmup=5):

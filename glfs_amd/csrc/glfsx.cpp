@@ -100,6 +100,17 @@ struct Ctx {
   PinBuf h_small, h_root;      // h_root: a root ref written by the kernels
   PinBuf h_oin, h_oct, h_oref;  // glfsx_post's one-shot staging
   PinBuf h_bin, h_bct, h_bref;  // glfsx_post_blobs' one-shot staging
+  // glfsx_post_blobs' small blobs from host memory: groups of <= 64 MiB
+  // through three pinned slots, upload / hash / download on three streams
+  struct BlobSlot {
+    PinBuf h_in, h_ct, h_meta, h_refs;  // h_meta: local offsets then lengths
+    DevBuf d_in, d_ct, d_meta, d_refs;
+    hipEvent_t done = nullptr, up = nullptr, hashed = nullptr;
+    uint64_t i0 = 0, i1 = 0;            // the group's blob index range
+    std::vector<uint64_t> loff;         // local offset of each blob in the range
+    bool busy = false;
+  } bslot[3];
+  hipStream_t s_up = nullptr, s_down = nullptr;
   // glfsx_post_tree_device: a second stream for the tree blob's posts, its
   // events, and the tree layout on the host
   hipStream_t stream2 = nullptr;
@@ -2515,6 +2526,169 @@ int capture_post(void *ctx, int kind, const uint8_t *ref, const void *ctext,
 }
 }  // namespace
 
+namespace {
+// glfsx_post_blobs' small blobs (<= small_max bytes), pipelined from host
+// memory: the blobs are taken in index order in groups whose bytes fit a
+// 64 MiB slot; each group's bytes are packed into pinned staging (runs of
+// blobs contiguous in `data` copied at once, by the copy pool), uploaded on
+// one stream, hashed one lane per blob (launch_post_small) on the context's
+// stream and their roots and ctext downloaded on a third, while the next
+// group is packed -- three slots in flight, so the host copy, both PCIe
+// directions and the kernels overlap.  A group's Posts are delivered when
+// its slot is reused or at the end, in blob order, the larger blobs' captured
+// Posts in their places: exactly n sequential PostBlob calls' order.
+constexpr uint64_t kGroupBytes = 64ull << 20;
+
+int complete_group(Ctx::BlobSlot &g, const uint64_t *lengths, uint64_t small_max,
+                   const std::vector<std::vector<CapturedPost>> &big, glfsx_post_fn post,
+                   void *post_ctx, uint8_t *roots_out) {
+  if (!g.busy) return 0;
+  HIP_TRY(hipEventSynchronize(g.done));
+  g.busy = false;
+  for (uint64_t i = g.i0; i < g.i1; ++i) {
+    if (lengths[i] <= small_max) {
+      const uint8_t *ref = g.h_refs.u8() + 64 * (i - g.i0);
+      memcpy(roots_out + 64 * i, ref, 64);
+      if (post) {
+        // a small blob's single Post: a data block, or the empty blob's
+        // index node (blob.go:187-189)
+        int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
+                      g.h_ct.u8() + g.loff[i - g.i0], lengths[i]);
+        if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+      }
+    } else if (post) {
+      for (const CapturedPost &p : big[i]) {
+        int rc = post(post_ctx, p.kind, p.ref, p.ctext.data(), p.ctext.size());
+        if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+      }
+    }
+  }
+  return 0;
+}
+
+int post_small_groups(Ctx *c, uint64_t bs, const uint8_t *salt, const uint8_t *cid_key,
+                      const uint8_t *data, const uint64_t *offsets, const uint64_t *lengths,
+                      uint64_t n, uint64_t small_max,
+                      const std::vector<std::vector<CapturedPost>> &big, glfsx_post_fn post,
+                      void *post_ctx, uint8_t *roots_out) {
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  if (!c->s_up) HIP_TRY(hipStreamCreateWithFlags(&c->s_up, hipStreamNonBlocking));
+  if (!c->s_down) HIP_TRY(hipStreamCreateWithFlags(&c->s_down, hipStreamNonBlocking));
+  for (auto &g : c->bslot)
+    if (!g.done) {
+      HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&g.up, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&g.hashed, hipEventDisableTiming));
+    }
+  // on any failure, nothing may still be writing the slots' pinned staging
+  auto drain = [&] {
+    for (hipStream_t st : {c->s_up, c->stream, c->s_down}) (void)hipStreamSynchronize(st);
+    for (auto &g : c->bslot) g.busy = false;
+  };
+  int k = 0;
+  uint64_t i = 0;
+  while (i < n) {
+    Ctx::BlobSlot &g = c->bslot[k];
+    k = (k + 1) % 3;
+    if (int e = complete_group(g, lengths, small_max, big, post, post_ctx, roots_out)) {
+      drain();
+      return e;
+    }
+    // the group: blobs [i, i1) whose small bytes fit kGroupBytes (a single
+    // blob always fits: small blobs are <= 16 KiB)
+    uint64_t i1 = i, bytes = 0, max_len = 0;
+    while (i1 < n) {
+      const uint64_t len = lengths[i1] <= small_max ? lengths[i1] : 0;
+      if (i1 > i && bytes + len > kGroupBytes) break;
+      bytes += len;
+      max_len = std::max(max_len, len);
+      ++i1;
+    }
+    const uint64_t m = i1 - i;
+    auto run = [&]() -> int {
+      if (int e = g.h_in.ensure(bytes + 64)) return e;
+      if (int e = g.d_in.ensure(bytes + 64)) return e;
+      if (int e = g.d_ct.ensure(bytes + 64)) return e;
+      if (post)
+        if (int e = g.h_ct.ensure(bytes + 64)) return e;
+      if (int e = g.h_meta.ensure(16 * m)) return e;
+      if (int e = g.d_meta.ensure(16 * m)) return e;
+      if (int e = g.h_refs.ensure(64 * m)) return e;
+      if (int e = g.d_refs.ensure(64 * m)) return e;
+      g.loff.assign(m, 0);
+      uint64_t *lo = reinterpret_cast<uint64_t *>(g.h_meta.p), *ll = lo + m;
+      // pack, copying each run of blobs that are contiguous in `data` at once
+      uint64_t o = 0, run_src = 0, run_dst = 0, run_len = 0;
+      for (uint64_t j = 0; j < m; ++j) {
+        const uint64_t idx = i + j, len = lengths[idx];
+        const bool small = len <= small_max;
+        lo[j] = small ? o : 0;
+        ll[j] = small ? len : kMaxSmallLen + 1;  // skipped by k_small
+        g.loff[j] = lo[j];
+        if (!small || len == 0) continue;
+        if (run_len && offsets[idx] == run_src + run_len && o == run_dst + run_len) {
+          run_len += len;
+        } else {
+          if (run_len) par_memcpy(g.h_in.u8() + run_dst, data + run_src, run_len);
+          run_src = offsets[idx];
+          run_dst = o;
+          run_len = len;
+        }
+        o += len;
+      }
+      if (run_len) par_memcpy(g.h_in.u8() + run_dst, data + run_src, run_len);
+      if (bytes) HIP_TRY(hipMemcpyAsync(g.d_in.p, g.h_in.p, bytes, hipMemcpyHostToDevice, c->s_up));
+      HIP_TRY(hipMemcpyAsync(g.d_meta.p, g.h_meta.p, 16 * m, hipMemcpyHostToDevice, c->s_up));
+      HIP_TRY(hipEventRecord(g.up, c->s_up));
+      HIP_TRY(hipStreamWaitEvent(c->stream, g.up, 0));
+      SmallJob j{};
+      j.src = g.d_in.u8();
+      j.ctext = g.d_ct.u8();
+      j.offs = reinterpret_cast<const uint64_t *>(g.d_meta.p);
+      j.lens = j.offs + m;
+      j.n = m;
+      j.max_len = max_len;
+      j.small_max = small_max;
+      j.refs = g.d_refs.u8();
+      words_from_key(j.raw_salt, salts.raw);
+      words_from_key(j.index_salt, salts.index);
+      if (cid_key) {
+        words_from_key(j.cid_key, cid_key);
+        j.cid_keyed = true;
+      } else {
+        blake3_iv_words(j.cid_key);
+      }
+      HIP_TRY(launch_post_small(j, c->stream));
+      HIP_TRY(hipEventRecord(g.hashed, c->stream));
+      HIP_TRY(hipStreamWaitEvent(c->s_down, g.hashed, 0));
+      HIP_TRY(hipMemcpyAsync(g.h_refs.p, g.d_refs.p, 64 * m, hipMemcpyDeviceToHost, c->s_down));
+      if (post && bytes)
+        HIP_TRY(hipMemcpyAsync(g.h_ct.p, g.d_ct.p, bytes, hipMemcpyDeviceToHost, c->s_down));
+      HIP_TRY(hipEventRecord(g.done, c->s_down));
+      return 0;
+    };
+    if (int e = run()) {
+      drain();
+      return e;
+    }
+    g.i0 = i;
+    g.i1 = i1;
+    g.busy = true;
+    i = i1;
+  }
+  // the rest, oldest first
+  for (int r = 0; r < 3; ++r) {
+    Ctx::BlobSlot &g = c->bslot[(k + r) % 3];
+    if (int e = complete_group(g, lengths, small_max, big, post, post_ctx, roots_out)) {
+      drain();
+      return e;
+    }
+  }
+  return 0;
+}
+}  // namespace
+
 int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
                      const uint8_t *cid_key, const void *data,
                      const uint64_t *offsets, const uint64_t *lengths, uint64_t n,
@@ -2527,23 +2701,18 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
     return fail(GLFSX_E_BLOCKSIZE_GT_MAX, "blockSize %llu > maxSize %llu",
                 (unsigned long long)bs, (unsigned long long)store_max);
   if (int e = check_block_size(bs)) return e;
-  // small blobs go through the device batch; single-block blobs of up to
-  // kMaxMedLen as one-shot posts, kMedBatchBytes at a time (their root is
-  // the block's ref, blob.go:190-193); larger ones Created one by one
-  // through the Writer.  The Posts of the latter two are captured and
-  // delivered in call order below.
-  std::vector<uint64_t> soffs(n), slens(n), med;
+  // small blobs go through the pipelined device batches (post_small_groups);
+  // single-block blobs of up to kMaxMedLen as one-shot posts, kMedBatchBytes
+  // at a time (their root is the block's ref, blob.go:190-193); larger ones
+  // Created one by one through the Writer.  The Posts of the latter two are
+  // captured and delivered in call order with the small blobs'.
+  std::vector<uint64_t> med;
   std::vector<std::vector<CapturedPost>> big(n);
-  uint64_t span = 0, max_len = 0, n_small = 0;
+  uint64_t n_small = 0;
   const uint64_t small_max = small_max_for(bs);  // one block, <= 16 KiB
   for (uint64_t i = 0; i < n; ++i) {
-    const bool small = lengths[i] <= small_max;
-    soffs[i] = offsets[i];
-    slens[i] = small ? lengths[i] : kMaxSmallLen + 1;  // skipped by k_small
-    if (small) {
+    if (lengths[i] <= small_max) {
       ++n_small;
-      span = std::max(span, offsets[i] + lengths[i]);
-      max_len = std::max(max_len, lengths[i]);
     } else if (lengths[i] <= bs && lengths[i] <= kMaxMedLen && one_enabled()) {
       med.push_back(i);
     } else {
@@ -2599,48 +2768,17 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
       g0 = g1;
     }
   }
-  std::vector<uint8_t> h_ct(post ? span + 1 : 0);
   if (n_small) {
-    if (int e = c->d_in.ensure(span + 64)) return e;
-    if (int e = c->d_ct.ensure(span + 64)) return e;
-    if (int e = c->d_refs.ensure(64 * n)) return e;
-    if (int e = c->d_lvl_a.ensure(16 * n)) return e;
-    c->d_lvl_a.dirty = SIZE_MAX;  // not an index-node image while in this use
-    uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_lvl_a.p);
-    uint64_t *d_len = d_off + n;
-    if (span)
-      HIP_TRY(hipMemcpyAsync(c->d_in.p, data, span, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_off, soffs.data(), 8 * n, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_len, slens.data(), 8 * n, hipMemcpyHostToDevice, c->stream));
-    if (int e = glfsx_post_blobs_device(bs, salt, cid_key, c->d_in.p, d_off, d_len, n,
-                                        max_len, c->d_ct.p, c->d_refs.p, c->stream))
+    if (int e = post_small_groups(c, bs, salt, cid_key, static_cast<const uint8_t *>(data),
+                                  offsets, lengths, n, small_max, big, post, post_ctx,
+                                  roots_out))
       return e;
-    std::vector<uint8_t> refs(64 * n);
-    HIP_TRY(hipMemcpyAsync(refs.data(), c->d_refs.p, 64 * n, hipMemcpyDeviceToHost,
-                           c->stream));
-    if (post && span)
-      HIP_TRY(hipMemcpyAsync(h_ct.data(), c->d_ct.p, span, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIP_TRY(stream_wait(c->stream));
+  } else if (post) {
     for (uint64_t i = 0; i < n; ++i)
-      if (lengths[i] <= small_max) memcpy(roots_out + 64 * i, &refs[64 * i], 64);
-  }
-  if (post) {
-    for (uint64_t i = 0; i < n; ++i) {
-      // one PostBlob per blob, in order: a small blob's single Post (a data
-      // block, or the empty index node, blob.go:187-189), or a large blob's
-      // whole Post sequence
-      if (lengths[i] <= small_max) {
-        int rc = post(post_ctx, lengths[i] ? 0 : 1, roots_out + 64 * i,
-                      h_ct.data() + offsets[i], lengths[i]);
+      for (const CapturedPost &p : big[i]) {
+        int rc = post(post_ctx, p.kind, p.ref, p.ctext.data(), p.ctext.size());
         if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
-      } else {
-        for (const CapturedPost &p : big[i]) {
-          int rc = post(post_ctx, p.kind, p.ref, p.ctext.data(), p.ctext.size());
-          if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
-        }
       }
-    }
   }
   return 0;
 }

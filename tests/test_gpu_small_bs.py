@@ -114,3 +114,47 @@ def test_post_tree_device_small_blob_block_size(gpu, O):
     want_tree, _, _, _ = O.create(bytes(lines[:t.value].cpu().numpy().tobytes()), 2 << 20,
                                   salt=tsalt, closed_form=True)
     assert bytes(r.ref) == want_tree
+
+
+def test_post_blobs_host_pipelined_groups(gpu, O):
+    """glfsx_post_blobs from host memory over several 64 MiB groups: 20000
+    blobs of 0..16 KiB at scattered (non-contiguous, unordered) offsets with
+    larger blobs between them (one-shot medium blobs and multi-block
+    Creates at bs = 2 MiB): every root and the whole Post log (kind, ref,
+    ctext) equal n sequential PostBlob calls of the oracle."""
+    import hashlib
+    import random
+    N = gpu
+    bs = 2 << 20
+    salt = O.derive_key(bytes(32), b"blob")
+    rng = random.Random(4)
+    lens = [rng.choice([0, 1, 4096, 4096, 4096, 8191, 16384, rng.randrange(16385)])
+            for _ in range(20000)]
+    for k in (17, 5000, 12345, 19999):
+        lens[k] = rng.choice([20000, 3 * bs + 5, bs])
+    order = list(range(len(lens)))
+    rng.shuffle(order)                 # blob bytes laid out in another order
+    offs = [0] * len(lens)
+    o = 0
+    for i in order:
+        offs[i] = o
+        o += lens[i] + rng.choice([0, 0, 3, 64])
+    data = O.fill_splitmix(o + 8, 6)
+    posts = []
+
+    @N.POST_FN
+    def sink(_ctx, kind, ref, ct, n):
+        posts.append((kind, ctypes.string_at(ref, 64), n,
+                      hashlib.sha256(ctypes.string_at(ct, n)).digest()))
+        return 0
+
+    n = len(lens)
+    roots = ctypes.create_string_buffer(64 * n)
+    N.check(N.lib.glfsx_post_blobs(bs, bs, salt, None, data, (ctypes.c_uint64 * n)(*offs),
+                                   (ctypes.c_uint64 * n)(*lens), n, sink, None, roots))
+    want_posts = []
+    for i in range(n):
+        r, _, _, ps = O.create(data[offs[i]:offs[i] + lens[i]], bs, salt=salt)
+        assert roots.raw[64 * i:64 * i + 64] == r, i
+        want_posts += [(k, ref, ln, hashlib.sha256(ct).digest()) for k, ref, ln, ct in ps]
+    assert posts == want_posts
