@@ -249,6 +249,9 @@ def main():
                 out["small_blobs"] = small_blobs(torch, N, stream, sp)
                 out["small_blobs_from_host"] = small_blobs_from_host(torch, N, stream, sp)
                 out["config4_end_to_end"] = config4_end_to_end(torch, N, stream, sp)
+                if world == 1 and "cpu_baseline" in out:
+                    out["cpu_baseline"].update(
+                        cpu_baseline_configs(args, out["config2"]["root_cid"]))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -689,6 +692,7 @@ def small_blobs_from_host(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
     stream.synchronize()
     host = d.cpu().numpy()
     want = roots_d.cpu().numpy().tobytes()
+    _GPU_REFS["small_blobs_seed0"] = want   # the CPU baseline checks its roots against these
     del d, roots_d, offs_d, lens_d
     offs = np.arange(n, dtype=np.uint64) * ln
     lens = np.full(n, ln, dtype=np.uint64)
@@ -720,6 +724,79 @@ def small_blobs_from_host(torch, N, stream, sp, n=1 << 20, ln=4096, reps=3):
                         "one lane per blob, roots + ctext D2H, every Post delivered in order "
                         "(native counting sink); roots_only: no sink, so no ctext download. "
                         "Roots equal the device batch's"})
+    return out
+
+
+_GPU_REFS = {}
+
+
+def cpu_baseline_configs(args, config2_root_cid):
+    """BASELINE.md section 2's other CPU baselines, the Go
+    path's primitive mix (oracle_post_batch_gomix: SIMD BLAKE3 + scalar
+    ChaCha20) on 1 core and on all cores of this job, each checked against
+    the GPU's results:
+      config2: BASELINE configs[1] -- a 1 GiB blob at 2 MiB blocks with the
+        glfs blob salt (splitmix seed 1): 512 data posts with rawSalt, the
+        index node with indexSalt (bigblob/ref.go:98-161, blob.go:165-206);
+        the root must equal config2's GPU root.
+      small_blobs: BASELINE config 4's hashing -- 1,048,576 x 4 KiB blobs
+        (blob i = splitmix seed i), root = post(rawSalt, blob)
+        (blob.go:190-193); 1 core over the first 262,144 blobs, all cores over
+        all of them; the roots must equal the GPU's."""
+    import hashlib
+    from oracle import oracle as O
+    L = O.lib()
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(),
+                       os.cpu_count()))
+    tsalt = O.derive_key(bytes(32), b"blob")            # machine.go:50-54
+    raw, idx = O.derive_key(tsalt, b"raw"), O.derive_key(tsalt, b"index")
+    out = {}
+    # config 2
+    size, bs = GIB, 2 * MIB
+    buf = ctypes.create_string_buffer(size)
+    ct = ctypes.create_string_buffer(size)
+    L.oracle_fill_splitmix(buf, 0, size, 1)
+    nb = size // bs
+    refs = ctypes.create_string_buffer(64 * nb)
+    c2 = {}
+    for label, th in (("one_core", 1), ("all_cores", cores)):
+        t = time.perf_counter()
+        rc = L.oracle_post_batch_gomix(refs, ct, raw, buf, size, bs, None, th)
+        root_ref, _ = O.post(idx, refs.raw.ljust(bs, b"\0"))   # the one index node
+        dt = time.perf_counter() - t
+        if rc not in (None, 0):
+            c2 = {"error": "no SIMD BLAKE3 in this image"}
+            break
+        c2[label] = {"value": round(size / GIB / dt, 4), "cores": th, "s": round(dt, 2)}
+        c2["root_equals_gpu"] = root_ref[:32].hex() == config2_root_cid
+    c2.update({"unit": "GiB/s", "kind": "port",
+               "sample": "the whole config: 1 GiB at 2 MiB blocks, 512 data posts + 1 index post"})
+    out["config2"] = c2
+    del buf, ct
+    # config 4's hashing
+    n, ln = 1 << 20, 4096
+    buf = ctypes.create_string_buffer(n * ln)
+    ct = ctypes.create_string_buffer(n * ln)
+    L.oracle_fill_splitmix_blobs(buf, n, ln, 0)
+    refs = ctypes.create_string_buffer(64 * n)
+    want = _GPU_REFS.get("small_blobs_seed0")
+    sb = {}
+    for label, th, m in (("one_core", 1, n // 4), ("all_cores", cores, n)):
+        t = time.perf_counter()
+        rc = L.oracle_post_batch_gomix(refs, ct, raw, buf, m * ln, ln, None, th)
+        dt = time.perf_counter() - t
+        if rc not in (None, 0):
+            sb = {"error": "no SIMD BLAKE3 in this image"}
+            break
+        got = refs.raw[:64 * m]
+        sb[label] = {"value": round(m * ln / GIB / dt, 4), "blobs_per_s": round(m / dt),
+                     "cores": th, "blobs": m, "s": round(dt, 2),
+                     "roots_equal_gpu": (None if want is None else
+                                         hashlib.sha256(got).digest() ==
+                                         hashlib.sha256(want[:64 * m]).digest())}
+    sb.update({"unit": "GiB/s", "kind": "port",
+               "sample": "one_core: the first 262,144 of the 1,048,576 blobs; all_cores: all"})
+    out["small_blobs"] = sb
     return out
 
 

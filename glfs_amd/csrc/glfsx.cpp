@@ -2871,7 +2871,15 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   hipStream_t B = c->stream2;
   const uint64_t wgs = (n + kTreeWG - 1) / kTreeWG;
   const uint64_t K = std::min(batches, wgs);
-  while (c->events.size() < K + 2) {
+  // K == 1: the lines' static parts are written on B beside the blobs' DEK
+  // pass and the CID pass writes each root's hex digits into its line
+  // (GLFSX_TREE_HEX=0: the lines kernel after the hashing, A/B)
+  static const bool hex_fused = [] {
+    const char *e = getenv("GLFSX_TREE_HEX");
+    return !e || atoi(e) != 0;
+  }();
+  const bool fuse = hex_fused && K == 1;
+  while (c->events.size() < K + 4) {
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->events.push_back(ev);
@@ -2880,7 +2888,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   if (int e = derive_salts(c, blob_salt, &bsalts)) return e;
   if (int e = derive_salts(c, tree_salt, &tsalts)) return e;
   const uint64_t words = n + wgs + 1;
-  if (int e = c->d_tree.ensure(8 * words)) return e;
+  if (int e = c->d_tree.ensure(8 * (words + (fuse ? n : 0)))) return e;
   if (int e = c->h_tree.ensure(8 * (wgs + 1))) return e;
   TreeJob tj{};
   tj.n = n;
@@ -2907,6 +2915,15 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   // exclusive prefix per entry workgroup, then the total (one copy)
   HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, A));
   HIP_TRY(hipEventRecord(c->events[K + 1], A));
+  hipEvent_t static_done = nullptr;
+  if (fuse) {
+    // B: the lines without their hex digits, and where each root's digits go
+    tj.hex_pos = tj.scratch + words;
+    HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
+    HIP_TRY(launch_tree_write(tj, 0, wgs, B));
+    static_done = c->events[K + 2];
+    HIP_TRY(hipEventRecord(static_done, B));
+  }
   SmallJob sj{};
   sj.src = static_cast<const uint8_t *>(d_data);
   sj.ctext = static_cast<uint8_t *>(d_ctext);
@@ -2929,8 +2946,15 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     sj.lens = d_lengths + e0;
     sj.n = e1 - e0;
     sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e0;
-    HIP_TRY(launch_post_small(sj, A));
-    HIP_TRY(launch_tree_write(tj, g0, g1, A));
+    if (fuse) {  // the CID pass writes the digits once the static parts are in
+      sj.hex_out = static_cast<uint8_t *>(d_lines);
+      sj.hex_pos = tj.hex_pos;
+      sj.cid_wait = static_done;
+      HIP_TRY(launch_post_small(sj, A));
+    } else {
+      HIP_TRY(launch_post_small(sj, A));
+      HIP_TRY(launch_tree_write(tj, g0, g1, A));
+    }
     HIP_TRY(hipEventRecord(c->events[b], A));
   }
   HIP_TRY(hipEventSynchronize(c->events[K + 1]));

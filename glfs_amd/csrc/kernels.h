@@ -82,6 +82,12 @@ struct SmallJob {
   // the blob block size) -- a longer blob has several blocks and an index
   // node (blob.go:120-206), so the caller Creates it (0 = kMaxSmallLen)
   uint64_t small_max;
+  // hex_out != nullptr: the CID pass also writes blob i's root as the tree
+  // line's hex fields -- 64 lower-case digits of the CID at hex_out +
+  // hex_pos[i] and of the DEK kDekAfterCid bytes later (TreeJob::hex_pos)
+  uint8_t *hex_out;
+  const uint64_t *hex_pos;
+  hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
 };
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
@@ -155,7 +161,15 @@ struct TreeJob {
   uint64_t *total;            // device word: total bytes
   uint8_t *out;               // nullable: lengths only
   uint64_t cap;               // bytes at out
+  // hex_pos != nullptr: k_tree_write leaves the 64 hex digits of each cid
+  // and dek unwritten and stores at hex_pos[i] the out offset of entry i's
+  // first cid digit (its dek digits start kDekAfterCid bytes later); the
+  // small-blob CID pass writes them (SmallJob::hex_out)
+  uint64_t *hex_pos;
 };
+// `<64 cid digits>","dek":"<64 dek digits>`: the dek's digits follow the
+// cid's first digit by 64 + len("\",\"dek\":\"") bytes
+constexpr uint32_t kDekAfterCid = 64 + 9;
 hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
 // The same in two steps: the layout (line lengths, per-workgroup exclusive
 // prefix at scratch + n, the total) -- it does not read the roots' values --

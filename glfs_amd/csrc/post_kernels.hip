@@ -1941,7 +1941,43 @@ struct SArgs {
   uint64_t n_coarse;  // k_small_q: items [0, n_coarse) are 64 blobs (one per
                       // lane); the blobs after them go as fine items
   uint64_t small_max;  // longer blobs are skipped (SmallJob::small_max)
+  uint8_t *hex_out;    // CID pass, nullable: the root as tree-line hex digits
+  const uint64_t *hex_pos;
 };
+
+// Lower-case hex digits of bytes 0 and 1 of x, in output order (hi(b0)
+// lo(b0) hi(b1) lo(b1)) as one little-endian word (tree_kernels.hip hex4).
+__device__ __forceinline__ uint32_t hex4(uint32_t x) {
+  const uint32_t n = ((x >> 4) & 0xFu) | ((x & 0xFu) << 8) |
+                     ((x >> 12) & 0xFu) << 16 | ((x >> 8) & 0xFu) << 24;
+  const uint32_t ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;  // nibble >= 10
+  return n + 0x30303030u + ge10 * 39u;
+}
+
+// The 64 hex digits of the 32 bytes in w (tree.go:309's "cid"/"dek" field
+// of a TreeEntry line, encoding as tree_kernels.hip's hex32) at dst, any
+// alignment: aligned 4-byte stores of the digits shifted into place
+// (alignbyte), the two partial words at the ends byte by byte -- no byte
+// outside [dst, dst + 64) is written.
+__device__ __forceinline__ void put_hex32(uint8_t *dst, const uint32_t w[8]) {
+  const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(dst) & 3u);
+  const uint32_t sh = 8u * (4u - s);  // s = 0: the whole next word
+  uint32_t *base = reinterpret_cast<uint32_t *>(dst - s);
+  uint32_t prev = 0;  // streamed one digit word at a time: few live values
+#pragma unroll
+  for (int k = 0; k <= 16; ++k) {
+    const uint32_t cur = k < 16 ? hex4(w[k >> 1] >> (16 * (k & 1))) : 0u;
+    const uint32_t v = uint32_t(((uint64_t(cur) << 32) | prev) >> sh);
+    if ((k >= 1 && k <= 15) || (k == 0 && s == 0)) {
+      base[k] = v;
+    } else {
+      const uint32_t lo = k == 0 ? s : 0u, hi = k == 0 ? 4u : s;
+      uint8_t *b = reinterpret_cast<uint8_t *>(base + k);
+      for (uint32_t x = lo; x < hi; ++x) b[x] = uint8_t(v >> (8u * x));
+    }
+    prev = cur;
+  }
+}
 
 // Blob i for the calling lane (nothing when i >= n); lds_u4: the
 // workgroup's 4 x 8 KiB staging images.  No barriers.
@@ -1994,6 +2030,13 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
     lane_subtree<G, CHACHA, false, A>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
   }
   store_digest(ref + a.out_off, cv);
+  if (CHACHA && a.hex_out) {  // the tree line's cid and dek digits
+    const uint64_t pos = a.hex_pos[i];
+    if (pos != ~0ull) {  // ~0: the lines did not fit their buffer
+      put_hex32(a.hex_out + pos, cv);
+      put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+    }
+  }
 }
 
 // A fine item of k_small_q: 64/G blobs, G lanes per blob (lane l hashes
@@ -2052,7 +2095,16 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
     }
     b3_compress<A>(cv, m, 0u, 0u, 64u, a.base | kParent | (2 * st == G ? kRoot : 0u));
   }
-  if (c == 0) store_digest(ref + a.out_off, cv);
+  if (c == 0) {
+    store_digest(ref + a.out_off, cv);
+    if (CHACHA && a.hex_out) {
+      const uint64_t pos = a.hex_pos[i];
+      if (pos != ~0ull) {
+        put_hex32(a.hex_out + pos, cv);
+        put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+      }
+    }
+  }
 }
 
 template <int G, bool CHACHA, int A = 2>
@@ -2997,6 +3049,12 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   for (int i = 0; i < 8; ++i) a.key[i] = a.key0[i] = job.cid_key[i];
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;
+  a.hex_out = job.hex_out;
+  a.hex_pos = job.hex_pos;
+  if (job.cid_wait) {  // e.g. the tree lines' static parts, on another stream
+    e = hipStreamWaitEvent(s, job.cid_wait, 0);
+    if (e != hipSuccess) return e;
+  }
   return launch_small_pass<true>(a, max_len, s);
 }
 

@@ -43,6 +43,7 @@ struct TArgs {
   uint8_t *out;
   uint64_t cap;         // bytes at out; nothing is written if the total exceeds it
   const uint64_t *total;
+  uint64_t *hex_pos;    // nullable: skip the hex digits, record where they go
 };
 
 constexpr uint32_t kImg = 60 * 1024;  // LDS image per workgroup
@@ -199,9 +200,13 @@ __device__ __forceinline__ uint32_t hex4(uint32_t x) {
 // "<64 hex digits>" of the 32 bytes at x (one 64-B ref holds two: aligned
 // refs are read as 16-B words)
 template <class S>
-__device__ __forceinline__ void hex32(S &k, const uint8_t *x, bool aligned) {
+__device__ __forceinline__ void hex32(S &k, const uint8_t *x, bool aligned, bool skip = false) {
   if constexpr (!S::kWrites) {
     k.o += 66;
+  } else if (skip) {  // the quotes only: the digits come from the CID pass
+    k.put('"');
+    k.o += 64;
+    k.put('"');
   } else {
     uint32_t w[8];
     if (aligned) {
@@ -234,8 +239,9 @@ __device__ __forceinline__ void hex32(S &k, const uint8_t *x, bool aligned) {
   }
 }
 
+// *cid_at: the offset in the line of the cid's first hex digit
 template <class S>
-__device__ uint32_t line(const TArgs &a, uint64_t i, S k) {
+__device__ uint32_t line(const TArgs &a, uint64_t i, S k, uint32_t *cid_at = nullptr) {
   lit(k, "{\"name\":");
   json_string(k, a.names + a.name_offs[i], a.name_offs[i + 1] - a.name_offs[i]);
   lit(k, ",\"mode\":");
@@ -244,9 +250,11 @@ __device__ uint32_t line(const TArgs &a, uint64_t i, S k) {
   json_string(k, a.types + a.type_offs[i], a.type_offs[i + 1] - a.type_offs[i]);
   const bool al = (reinterpret_cast<uintptr_t>(a.roots) & 15) == 0;
   lit(k, ",\"cid\":");
-  hex32(k, a.roots + 64 * i, al);
+  const bool skip = a.hex_pos != nullptr;
+  if (cid_at) *cid_at = k.o + 1;
+  hex32(k, a.roots + 64 * i, al, skip);
   lit(k, ",\"dek\":");
-  hex32(k, a.roots + 64 * i + 32, al);
+  hex32(k, a.roots + 64 * i + 32, al, skip);
   lit(k, ",\"size\":");
   dec(k, a.sizes[i]);
   lit(k, ",\"blockSize\":");
@@ -308,16 +316,27 @@ __global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a, uint32_t wg0) {
   const uint64_t base = a.wg_total[wg];           // exclusive prefix
   const uint64_t span = a.local_end[last];        // this workgroup's bytes
   const uint32_t sh = uint32_t((reinterpret_cast<uintptr_t>(a.out) + base) & 15);
-  if (*a.total > a.cap) return;  // uniform: the caller reports the error
+  if (*a.total > a.cap) {  // uniform: the caller reports the error
+    // and the CID pass must not write digits anywhere
+    if (a.hex_pos && i < a.n) a.hex_pos[i] = ~0ull;
+    return;
+  }
   const uint64_t end = i < a.n ? a.local_end[i] : 0;
   const uint64_t start = (i < a.n && threadIdx.x) ? a.local_end[i - 1] : 0;
   if (i < a.n && a.line_ends) a.line_ends[i] = base + end;
+  uint32_t cid_at = 0;
   if (span + sh > kImg) {  // uniform: lines too long for the image
-    if (i < a.n) line(a, i, GlobalSink{a.out + base + start, 0});
+    if (i < a.n) {
+      line(a, i, GlobalSink{a.out + base + start, 0}, &cid_at);
+      if (a.hex_pos) a.hex_pos[i] = base + start + cid_at;
+    }
     return;
   }
-  if (i < a.n)
-    line(a, i, LdsSink{(__attribute__((address_space(3))) uint8_t *)img + sh + start, 0});
+  if (i < a.n) {
+    line(a, i, LdsSink{(__attribute__((address_space(3))) uint8_t *)img + sh + start, 0},
+         &cid_at);
+    if (a.hex_pos) a.hex_pos[i] = base + start + cid_at;
+  }
   __syncthreads();
   // image byte x <-> out byte base - sh + x; granules [16g, 16g+16)
   uint8_t *dst = a.out + base - sh;
@@ -373,6 +392,7 @@ TArgs tree_args(const TreeJob &j) {
   a.out = j.out;
   a.cap = j.cap;
   a.total = j.total;
+  a.hex_pos = j.hex_pos;
   return a;
 }
 }  // namespace
