@@ -367,7 +367,8 @@ def multi_lane_host(torch, N, args, devs, bs):
     never the headline value."""
     import numpy as np
     nd = len(devs)
-    n = int(min(args.host_rt_gib, 4.0) * GIB) // bs * bs * nd
+    # 4 GiB per GPU up to 16 GiB in all (the legs stay within a minute at N = 8)
+    n = int(min(args.host_rt_gib * nd, 4.0 * nd, 16.0) * GIB) // bs * bs
     host = host_stream(torch, N, n, args.seed)
     store_post = ctypes.cast(N.lib.glfsx_store_post, N.POST_FN)
     root = N.glfsx_root()

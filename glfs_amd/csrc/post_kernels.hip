@@ -2373,6 +2373,7 @@ uint32_t split_target_default() {
 }
 std::atomic<uint32_t> g_split_target{split_target_default()};
 constexpr uint32_t kMaxSplitLog2 = 8;  // the last workgroup merges <= 256 CVs
+constexpr uint64_t kDcMinWgs = 1024;   // see pass_plan
 
 // Split-mode scratch (32 B per workgroup) and arrival counters (4 B per
 // message, zero between launches: each message's last workgroup resets its
@@ -2577,9 +2578,33 @@ void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   // few messages: halve the chunks per lane and double the workgroups per
   // message until the launch fills the chip (256 CUs x 8 workgroups)
   const uint64_t target = g_split_target.load(std::memory_order_relaxed);
+  const int g0 = g;
+  const uint32_t sl0 = sl;
   while (g > 1 && sl < kMaxSplitLog2 && (n << sl) < target) {
     g /= 2;
     ++sl;
+  }
+  // ... but a one-launch split post (k_pass_dc: more than latency_wgs * 5/8
+  // workgroups, G <= 4) of fewer than ~1024 workgroups runs its DEK and CID
+  // items in about one round each and loses to the two-pass latency form:
+  // take the plan with the most workgroups that stays in that form.  Create
+  // at 2 MiB blocks, 64 / 115 blocks (the config-4 tree blob): 355 -> 499 /
+  // 546 -> 590 GiB/s; 128 x 1 MiB 362 -> 506; 200 x 2 MiB and up, or 256 x
+  // 1 MiB and up, keep the one-launch plan (scripts/r4_plan_sweep.py,
+  // DESIGN.md section 5)
+  const uint64_t lat = uint64_t(g_latency_wgs.load(std::memory_order_relaxed)) * 5 / 8;
+  if (sl > 0 && g <= 4 && (n << sl) > lat && (n << sl) < kDcMinWgs) {
+    int bg = 0;
+    uint32_t bsl = 0;
+    for (int gg = g0, s = int(sl0); gg >= 1 && s <= int(kMaxSplitLog2); gg /= 2, ++s)
+      if ((n << s) <= lat) {
+        bg = gg;
+        bsl = uint32_t(s);
+      }
+    if (bg && bsl > 0) {
+      g = bg;
+      sl = bsl;
+    }
   }
   *g_out = g;
   *sl_out = sl;

@@ -144,6 +144,27 @@ __device__ __forceinline__ void put_ascii(S &k, uint32_t b) {
 
 template <class S>
 __device__ void json_string(S &k, const uint8_t *s, uint64_t n) {
+  // Short strings (names like config 4's "%07d", types): every byte's load
+  // in flight at once, then the bytes from registers -- the general loop
+  // below waits for each byte's load before the next (its step depends on
+  // the byte), a chain of ~11 dependent global loads per line that left the
+  // line kernels latency-bound at two workgroups per CU.
+  if (n <= 16) {
+    uint32_t b[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) b[q] = uint64_t(q) < n ? s[q] : 0u;
+    uint32_t hi = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) hi |= b[q];
+    if (hi < 0x80) {  // ASCII: no rune decoding
+      k.put('"');
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (uint64_t(q) < n) put_ascii(k, b[q]);
+      k.put('"');
+      return;
+    }
+  }
   k.put('"');
   for (uint64_t i = 0; i < n;) {
     const uint8_t b = s[i];

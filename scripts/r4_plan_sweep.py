@@ -17,7 +17,14 @@ GIB, MIB = 1 << 30, 1 << 20
 m = glfs.Machine()
 shapes = {"tree_blob": (241172480, 2 * MIB, m.make_salt("tree")),
           "config2": (GIB, 2 * MIB, m.make_salt("blob"))}
-targets = [int(x) for x in (sys.argv[1:] or ["2048", "1024", "512", "400", "256", "128"])]
+args = sys.argv[1:]
+if args and args[0] == "--shapes":   # --shapes NxBS,NxBS,... (blocks x block size)
+    shapes = {}
+    for sh in args[1].split(","):
+        nb, bs = (int(x) for x in sh.split("x"))
+        shapes[f"{nb}x{bs >> 10}K"] = (nb * bs, bs, m.make_salt("blob"))
+    args = args[2:]
+targets = [int(x) for x in (args or ["2048", "1024", "512", "400", "256", "128"])]
 stream = torch.cuda.Stream()
 sp = ctypes.c_void_p(stream.cuda_stream)
 res = {k: {t: [] for t in targets} for k in shapes}
