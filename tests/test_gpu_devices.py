@@ -49,14 +49,15 @@ def test_writer_distinct_devices_4gib_stream(gpu, stream4g):  # noqa: F811
 def test_writer_distinct_devices_fused_failure_on_home_lane(gpu, O):
     """a failed one-launch post (k_pass_dc DEK wait) in a batch
     on the home lane, completed while the other lane's device is current,
-    must be seen and the batches in flight hashed again -- 96 MiB batches
-    over lanes [0, 1], the first batch (home, device 0) faulted."""
+    must be seen and the batches in flight hashed again -- 256 MiB batches
+    (fused launches) over lanes [0, 1], the first batch (home, device 0)
+    faulted; it completes when the sixth batch (lane 1) is submitted."""
     N = gpu
-    bs, total = MIB, 700 * MIB + 5
+    bs, total = MIB, 6 * 256 * MIB + 5
     data = O.fill_splitmix(total, 13)
     want_root, want_log = _oracle_post_log(O, data, bs)
     old = os.environ.get("GLFSX_BATCH_MIB")
-    os.environ["GLFSX_BATCH_MIB"] = "96"
+    os.environ["GLFSX_BATCH_MIB"] = "256"
     try:
         before = N.lib.glfsx_debug_fused(50, 2000)
         root, log = _gpu_post_log(N, data, bs, [0, 1], 64 * MIB)

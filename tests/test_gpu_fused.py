@@ -43,13 +43,15 @@ def _create_device(N, t, size, bs, salt=None):
 
 
 def test_fused_timeout_create_device_repeats(gpu, O, fused_fault):
-    """96 MiB at 1 MiB = 96 blocks x 4 workgroups: one fused launch.  Block 5's
-    DEK flag is withheld; the CID items of block 5 time out after 2 ms, the
-    host sees the error word and repeats the Create with two launches: the
-    root equals the oracle's, one failure is counted."""
+    """257 MiB at 1 MiB = 257 blocks x 4 workgroups: one fused launch (a
+    launch of fewer than 1024 workgroups takes the two-pass latency form,
+    pass_plan).  Block 5's DEK flag is withheld; the CID items of block 5
+    time out after 2 ms, the host sees the error word and repeats the Create
+    with two launches: the root equals the oracle's, one failure is
+    counted."""
     torch = _torch()
     from glfs_amd import _native as N
-    size, bs = 96 * MIB + 4096, MIB
+    size, bs = 256 * MIB + 4096, MIB
     t = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
     N.check(N.lib.glfsx_fill_splitmix_device(t.data_ptr(), 0, size, 77, None))
     torch.cuda.synchronize()
@@ -67,7 +69,7 @@ def test_fused_timeout_post_batch_repeats(gpu, O, fused_fault):
     """glfsx_post_batch (host buffers): the faulted slab is posted again;
     every ref and ctext byte equals the oracle."""
     from glfs_amd import _native as N
-    bs, total = MIB, 100 * MIB + 333
+    bs, total = MIB, 256 * MIB + 333       # a 256-block fused slab + 1 block
     salt = bytes(range(32))
     data = O.fill_splitmix(total, 3)
     before = fused_fault(7, 2000)
@@ -83,11 +85,12 @@ def test_fused_timeout_post_batch_repeats(gpu, O, fused_fault):
 
 
 def test_fused_timeout_writer_rehashes(gpu, O, fused_fault):
-    """The Writer with 96-block batches (GLFSX_BATCH_MIB=96): the first
-    batch's fused launch fails; every batch in flight is hashed again and the
-    Post log (kind, ref, ctext) and root equal the oracle writer's."""
+    """The Writer with 256-block batches (GLFSX_BATCH_MIB=256, fused
+    launches): the first batch's fused launch fails; every batch in flight
+    is hashed again and the Post log (kind, ref, ctext) and root equal the
+    oracle writer's."""
     from glfs_amd import _native as N
-    bs, total = MIB, 300 * MIB + 5
+    bs, total = MIB, 600 * MIB + 5
     data = O.fill_splitmix(total, 11)
     want_root, _, _, want_posts = O.create(data, bs)
     got = []
@@ -98,7 +101,7 @@ def test_fused_timeout_writer_rehashes(gpu, O, fused_fault):
         return 0
 
     old = os.environ.get("GLFSX_BATCH_MIB")
-    os.environ["GLFSX_BATCH_MIB"] = "96"
+    os.environ["GLFSX_BATCH_MIB"] = "256"
     try:
         before = fused_fault(50, 2000)
         root = N.glfsx_root()
