@@ -2871,8 +2871,8 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   hipStream_t B = c->stream2;
   const uint64_t wgs = (n + kTreeWG - 1) / kTreeWG;
   const uint64_t K = std::min(batches, wgs);
-  // K == 1: the blobs' DEK pass writes each line's static parts and the CID
-  // pass each root's hex digits into its line -- no lines kernel
+  // K == 1: the lines' static parts are written on B beside the blobs' DEK
+  // pass and the CID pass writes each root's hex digits into its line
   // (GLFSX_TREE_HEX=0: the lines kernel after the hashing, A/B)
   static const bool hex_fused = [] {
     const char *e = getenv("GLFSX_TREE_HEX");
@@ -2915,7 +2915,15 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   // exclusive prefix per entry workgroup, then the total (one copy)
   HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, A));
   HIP_TRY(hipEventRecord(c->events[K + 1], A));
-  if (fuse) tj.hex_pos = tj.scratch + words;  // where each root's digits go
+  hipEvent_t static_done = nullptr;
+  if (fuse) {
+    // B: the lines without their hex digits, and where each root's digits go
+    tj.hex_pos = tj.scratch + words;
+    HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
+    HIP_TRY(launch_tree_write(tj, 0, wgs, B));
+    static_done = c->events[K + 2];
+    HIP_TRY(hipEventRecord(static_done, B));
+  }
   SmallJob sj{};
   sj.src = static_cast<const uint8_t *>(d_data);
   sj.ctext = static_cast<uint8_t *>(d_ctext);
@@ -2938,24 +2946,10 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     sj.lens = d_lengths + e0;
     sj.n = e1 - e0;
     sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e0;
-    if (fuse) {  // the DEK pass writes the static parts, the CID pass the digits
-      TreeLineArgs &L = sj.lines;
-      L.names = tj.names;
-      L.name_offs = tj.name_offs;
-      L.modes = tj.modes;
-      L.types = tj.types;
-      L.type_offs = tj.type_offs;
-      L.roots = tj.roots;
-      L.sizes = tj.sizes;
-      L.block_sizes = tj.block_sizes;
-      L.local_end = tj.scratch;
-      L.wg_total = tj.scratch + n;
-      L.total = tj.total;
-      L.cap = tj.cap;
-      L.out = tj.out;
-      L.hex_pos = tj.hex_pos;
+    if (fuse) {  // the CID pass writes the digits once the static parts are in
       sj.hex_out = static_cast<uint8_t *>(d_lines);
       sj.hex_pos = tj.hex_pos;
+      sj.cid_wait = static_done;
       HIP_TRY(launch_post_small(sj, A));
     } else {
       HIP_TRY(launch_post_small(sj, A));

@@ -70,27 +70,6 @@ hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
 constexpr uint64_t kMaxSmallLen = 16ull * 1024;
 // entries per workgroup of the tree-line kernels (tree_kernels.hip)
 constexpr uint32_t kTreeWG = 256;
-// What the small-blob DEK pass writes of each blob's tree line
-// (glfsx_post_tree_device): line i's static parts -- everything but the 64
-// cid and 64 dek digits -- at its place in `out` (the layout of
-// launch_tree_layout: wg_total = exclusive prefix per kTreeWG entries,
-// local_end = inclusive end within them), and in hex_pos[i] where its cid
-// digits go (~0 when the lines exceed cap: nothing is written then).  The
-// CID pass writes the digits (SmallJob::hex_out).  out == nullptr: none.
-struct TreeLineArgs {
-  const uint8_t *names;
-  const uint64_t *name_offs;  // n + 1
-  const uint32_t *modes;
-  const uint8_t *types;
-  const uint64_t *type_offs;  // n + 1
-  const uint8_t *roots;       // not read (the digits are skipped)
-  const uint64_t *sizes, *block_sizes;
-  const uint64_t *local_end, *wg_total;
-  const uint64_t *total;
-  uint64_t cap;
-  uint8_t *out;
-  uint64_t *hex_pos;
-};
 struct SmallJob {
   const uint8_t *src;
   uint8_t *ctext;  // nullable; same offsets as src
@@ -108,7 +87,7 @@ struct SmallJob {
   // hex_pos[i] and of the DEK kDekAfterCid bytes later (TreeJob::hex_pos)
   uint8_t *hex_out;
   const uint64_t *hex_pos;
-  TreeLineArgs lines;  // DEK pass: the tree lines' static parts (out nullable)
+  hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
 };
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }

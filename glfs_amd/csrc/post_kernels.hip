@@ -20,7 +20,6 @@
 //     ptext is read once per pass and ctext is never re-read.
 // Integer ALU work only (v_add3_u32 / v_xor_b32 / v_alignbit_b32); no MFMA.
 #include "kernels.h"
-#include "tree_line.h"
 
 #include <algorithm>
 #include <atomic>
@@ -1944,25 +1943,15 @@ struct SArgs {
   uint64_t small_max;  // longer blobs are skipped (SmallJob::small_max)
   uint8_t *hex_out;    // CID pass, nullable: the root as tree-line hex digits
   const uint64_t *hex_pos;
-  TreeLineArgs ln;     // DEK pass: the tree lines' static parts (ln.out nullable)
 };
 
-using tree_line::hex4;
-
-// The DEK pass's epilogue for blob i when its tree line is wanted
-// (glfsx_post_tree_device): the line's static parts written straight to
-// their place (byte stores: ~100 per blob, beside 4 KiB of hashing) and
-// where its digits go, for the CID pass.
-__device__ __noinline__ void dek_line(const TreeLineArgs &L, uint64_t i) {
-  uint64_t pos = ~0ull;
-  if (*L.total <= L.cap) {
-    const uint64_t w = i / kTreeWG, r = i % kTreeWG;
-    const uint64_t start = L.wg_total[w] + (r ? L.local_end[i - 1] : 0);
-    uint32_t cid_at = 0;
-    tree_line::line(L, i, tree_line::GlobalSink{L.out + start, 0}, &cid_at);
-    pos = start + cid_at;
-  }
-  L.hex_pos[i] = pos;
+// Lower-case hex digits of bytes 0 and 1 of x, in output order (hi(b0)
+// lo(b0) hi(b1) lo(b1)) as one little-endian word (tree_kernels.hip hex4).
+__device__ __forceinline__ uint32_t hex4(uint32_t x) {
+  const uint32_t n = ((x >> 4) & 0xFu) | ((x & 0xFu) << 8) |
+                     ((x >> 12) & 0xFu) << 16 | ((x >> 8) & 0xFu) << 24;
+  const uint32_t ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;  // nibble >= 10
+  return n + 0x30303030u + ge10 * 39u;
 }
 
 // The 64 hex digits of the 32 bytes in w (tree.go:309's "cid"/"dek" field
@@ -2041,7 +2030,6 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
     lane_subtree<G, CHACHA, false, A>(cv, msg, cmsg, len, 0u, C, true, key, a.base, dek);
   }
   store_digest(ref + a.out_off, cv);
-  if (!CHACHA && a.ln.out) dek_line(a.ln, i);  // the tree line's static parts
   if (CHACHA && a.hex_out) {  // the tree line's cid and dek digits
     const uint64_t pos = a.hex_pos[i];
     if (pos != ~0ull) {  // ~0: the lines did not fit their buffer
@@ -2109,7 +2097,6 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
   }
   if (c == 0) {
     store_digest(ref + a.out_off, cv);
-    if (!CHACHA && a.ln.out) dek_line(a.ln, i);
     if (CHACHA && a.hex_out) {
       const uint64_t pos = a.hex_pos[i];
       if (pos != ~0ull) {
@@ -3082,15 +3069,17 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   }
   a.base = kKeyed;
   a.out_off = 32;
-  a.ln = job.lines;
   hipError_t e = launch_small_pass<false>(a, max_len, s);
   if (e != hipSuccess) return e;
   for (int i = 0; i < 8; ++i) a.key[i] = a.key0[i] = job.cid_key[i];
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;
-  a.ln = TreeLineArgs{};
   a.hex_out = job.hex_out;
   a.hex_pos = job.hex_pos;
+  if (job.cid_wait) {  // e.g. the tree lines' static parts, on another stream
+    e = hipStreamWaitEvent(s, job.cid_wait, 0);
+    if (e != hipSuccess) return e;
+  }
   return launch_small_pass<true>(a, max_len, s);
 }
 
