@@ -2920,7 +2920,14 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     // B: the lines without their hex digits, and where each root's digits go
     tj.hex_pos = tj.scratch + words;
     HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
-    HIP_TRY(launch_tree_write(tj, 0, wgs, B));
+    static const bool half = [] {  // GLFSX_TREE_HALF=0: full workgroups (A/B)
+      const char *e = getenv("GLFSX_TREE_HALF");
+      return !e || atoi(e) != 0;
+    }();
+    if (half)
+      HIP_TRY(launch_tree_static(tj, B));
+    else
+      HIP_TRY(launch_tree_write(tj, 0, wgs, B));
     static_done = c->events[K + 2];
     HIP_TRY(hipEventRecord(static_done, B));
   }

@@ -176,6 +176,9 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
 // and the lines of entry workgroups [wg0, wg1) (kTreeWG entries each).
 hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s);
 hipError_t launch_tree_write(const TreeJob &j, uint64_t wg0, uint64_t wg1, hipStream_t s);
+// The lines without their hex digits (j.hex_pos set), in half workgroups
+// small enough to run beside the small-blob DEK pass.
+hipError_t launch_tree_static(const TreeJob &j, hipStream_t s);
 
 // n blobs of len bytes (len % 8 == 0), blob b = the splitmix stream of seed
 // seed0 + b (see oracle_fill_splitmix_blobs).

@@ -373,6 +373,63 @@ __global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a, uint32_t wg0) {
   }
 }
 
+// The static lines of glfsx_post_tree_device (hex_pos set: the digits come
+// from the CID pass) in half workgroups: 128 threads for the entries [h *
+// 128, h * 128 + 128) of layout workgroup wg (block 2 wg + h), a 30 KiB
+// image.  Sized to run beside the small-blob DEK pass, whose persistent
+// workgroups hold 4 x 32 KiB of each CU's 160 KiB LDS and 4 x 112 of each
+// SIMD's 512 VGPRs per lane: this one (~50 VGPRs, one wave per SIMD) fits in
+// what they leave, so the lines are written while the blobs hash instead
+// of after (the 60 KiB form only got CUs as the DEK pass drained).
+constexpr uint32_t kHalf = kTreeWG / 2;
+constexpr uint32_t kHalfImg = 30 * 1024;
+__global__ __launch_bounds__(kHalf) void k_tree_write_half(TArgs a) {
+  __shared__ uint4 img4[kHalfImg / 16];
+  uint8_t *img = reinterpret_cast<uint8_t *>(img4);
+  const uint64_t wg = blockIdx.x >> 1, h = blockIdx.x & 1u;
+  const uint64_t e0 = wg * kTreeWG + h * kHalf;  // this half's first entry
+  const uint64_t i = e0 + threadIdx.x;
+  if (e0 >= a.n) return;  // uniform: an empty second half
+  if (*a.total > a.cap) {  // uniform: the caller reports the error
+    if (i < a.n) a.hex_pos[i] = ~0ull;  // and the CID pass writes nothing
+    return;
+  }
+  const uint64_t last = min<uint64_t>(e0 + kHalf, a.n) - 1;
+  const uint64_t p0 = h ? a.local_end[e0 - 1] : 0;  // the half's start in its workgroup
+  const uint64_t base = a.wg_total[wg] + p0;
+  const uint64_t span = a.local_end[last] - p0;
+  const uint32_t sh = uint32_t((reinterpret_cast<uintptr_t>(a.out) + base) & 15);
+  const uint64_t start = (i < a.n && i > e0) ? a.local_end[i - 1] - p0 : 0;
+  if (i < a.n && a.line_ends) a.line_ends[i] = base + a.local_end[i] - p0;
+  uint32_t cid_at = 0;
+  if (span + sh > kHalfImg) {  // uniform: lines too long for the image
+    if (i < a.n) {
+      line(a, i, GlobalSink{a.out + base + start, 0}, &cid_at);
+      a.hex_pos[i] = base + start + cid_at;
+    }
+    return;
+  }
+  if (i < a.n) {
+    line(a, i, LdsSink{(__attribute__((address_space(3))) uint8_t *)img + sh + start, 0},
+         &cid_at);
+    a.hex_pos[i] = base + start + cid_at;
+  }
+  __syncthreads();
+  // image byte x <-> out byte base - sh + x; the partial granules at the
+  // ends are shared with the neighbouring half and written byte by byte
+  uint8_t *dst = a.out + base - sh;
+  const uint32_t tot = uint32_t(span) + sh;
+  const uint32_t ng = (tot + 15) / 16;
+  for (uint32_t g = threadIdx.x; g < ng; g += kHalf) {
+    const uint32_t lo = 16 * g, hi = lo + 16;
+    if (lo >= sh && hi <= tot) {
+      *reinterpret_cast<uint4 *>(dst + lo) = img4[g];
+    } else {
+      for (uint32_t x = max(lo, sh); x < min(hi, tot); ++x) dst[x] = img[x];
+    }
+  }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -426,6 +483,14 @@ hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs, j.total);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_static(const TreeJob &j, hipStream_t s) {
+  if (j.n == 0 || !j.out || !j.hex_pos) return hipErrorInvalidValue;
+  const uint64_t wgs = (j.n + kTreeWG - 1) / kTreeWG;
+  hipLaunchKernelGGL(k_tree_write_half, dim3(uint32_t(2 * wgs)), dim3(kHalf), 0, s,
+                     tree_args(j));
   return hipGetLastError();
 }
 
