@@ -2373,7 +2373,11 @@ uint32_t split_target_default() {
 }
 std::atomic<uint32_t> g_split_target{split_target_default()};
 constexpr uint32_t kMaxSplitLog2 = 8;  // the last workgroup merges <= 256 CVs
-constexpr uint64_t kDcMinWgs = 1024;   // see pass_plan
+// see pass_plan; GLFSX_DC_MIN overrides (0: the round-3 plans, A/B)
+const uint64_t kDcMinWgs = [] {
+  const char *e = getenv("GLFSX_DC_MIN");
+  return e ? uint64_t(strtoull(e, nullptr, 10)) : uint64_t(1024);
+}();
 
 // Split-mode scratch (32 B per workgroup) and arrival counters (4 B per
 // message, zero between launches: each message's last workgroup resets its
