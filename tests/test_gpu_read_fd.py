@@ -164,3 +164,32 @@ def test_read_at_callback_and_python_file_route(gpu, O, file300):
         assert f.tell() == len(data)
     assert r2.ref.marshal_binary() == _oracle_post_log(O, data[17:], MIB)[0]
     assert r2.size == len(data) - 17
+
+
+def test_read_at_short_reads_and_strict(gpu, O, file300):
+    """A ReaderAt that returns at most 100,003 bytes per call (short reads at
+    every piece boundary, as a network-backed io.ReaderAt may) into a strict
+    writer over two lanes of the one GPU: the Post log equals the oracle's."""
+    N = gpu
+    path, data = file300
+    n = 97 * MIB + 11
+    want_root, want_log = _oracle_post_log(O, data[:n], MIB)
+    sink, log = _sink_log(N)
+    w = _writer(N, MIB, sink, [0, 0])
+    N.check(N.lib.glfsx_writer_set_strict(w, 1))
+    mv = memoryview(data)
+
+    def short(_ctx, buf, ln, off):
+        k = max(0, min(ln, 100_003, n - off))
+        ctypes.memmove(buf, bytes(mv[off:off + k]), k)
+        return k
+    cb = N.READ_AT_FN(short)
+    try:
+        got = ctypes.c_uint64()
+        rc = N.lib.glfsx_writer_read_at(w, cb, None, 0, (1 << 64) - 1, ctypes.byref(got))
+        N.check(rc, (N.lib.glfsx_writer_error(w) or b"").decode())
+        assert got.value == n
+        assert _finish(N, w) == want_root
+    finally:
+        N.lib.glfsx_writer_free(w)
+    assert log == want_log

@@ -158,3 +158,42 @@ def test_post_blobs_host_pipelined_groups(gpu, O):
         assert roots.raw[64 * i:64 * i + 64] == r, i
         want_posts += [(k, ref, ln, hashlib.sha256(ct).digest()) for k, ref, ln, ct in ps]
     assert posts == want_posts
+
+
+@pytest.mark.parametrize("fail_at", [1, 7, 20001])
+def test_post_blobs_host_store_error_stops_in_order(gpu, O, fail_at):
+    """glfsx_post_blobs from host memory with a store whose fail_at-th Post
+    fails (the first group, a later one, past a multi-block blob): the call
+    returns GLFSX_E_STORE and the store saw exactly the sequential PostBlob
+    calls' Posts up to the failing one (blob.go:153-156: the first failing
+    Post in order is returned, none after it)."""
+    import hashlib
+    N = gpu
+    bs = 2 << 20
+    salt = O.derive_key(bytes(32), b"blob")
+    lens = [4096] * 20000 + [3 * bs + 5] + [4096] * 30000   # > 64 MiB of small blobs
+    offs, o = [], 0
+    for ln in lens:
+        offs.append(o)
+        o += ln
+    data = O.fill_splitmix(o + 8, 17)
+    log = []
+
+    @N.POST_FN
+    def sink(_ctx, kind, ref, ct, n):
+        log.append((kind, ctypes.string_at(ref, 64), n, hashlib.sha256(ctypes.string_at(ct, n)).digest()))
+        return 1 if len(log) == fail_at else 0
+
+    n = len(lens)
+    roots = ctypes.create_string_buffer(64 * n)
+    rc = N.lib.glfsx_post_blobs(bs, bs, salt, None, data, (ctypes.c_uint64 * n)(*offs),
+                                (ctypes.c_uint64 * n)(*lens), n, sink, None, roots)
+    assert rc == N.GLFSX_E_STORE
+    assert len(log) == fail_at
+    want = []
+    i = 0
+    while len(want) < fail_at:
+        _, _, _, ps = O.create(data[offs[i]:offs[i] + lens[i]], bs, salt=salt)
+        want += [(k, r, ln, hashlib.sha256(c).digest()) for k, r, ln, c in ps]
+        i += 1
+    assert log == want[:fail_at]
