@@ -116,8 +116,14 @@ def main():
     except ValueError as e:
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         sys.exit(2)
+    # host buffers, the tmpfs file and the library's copy threads on the
+    # GPU's NUMA node (file feed 27-29 -> 35-39 GiB/s on a two-socket box;
+    # DESIGN.md section 8); a one-process run over GPUs on both sockets
+    # stays unbound
+    nodes = {gpu_numa_node(torch, d) for d in devs}
+    host_node = numa_bind(torch, devs[0]) if len(nodes) == 1 else None
     if mode == "one_process":
-        return main_one_process(args, devs)
+        return main_one_process(args, devs, host_node)
     dev = devs[0]
     torch.cuda.set_device(dev)
     N.set_device(dev)
@@ -202,6 +208,7 @@ def main():
                    "posts_per_step": n_posts.value if world == 1 else None,
                    "parallelism": f"disjoint block ranges x{world}"},
         "root_cid": root_ref[0][:32].hex() if rank == 0 else None,
+        "host_numa_node": host_node,
     }
 
     if not args.no_extras:
@@ -258,7 +265,41 @@ def main():
         dist.destroy_process_group()
 
 
-def main_one_process(args, devs):
+def gpu_numa_node(torch, dev):
+    """The NUMA node of GPU `dev` (sysfs of its PCI function), or None."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+        return node if node >= 0 else None
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
+def numa_bind(torch, dev):
+    """Run this process (and the threads it starts later, e.g. the
+    library's copy pool) on the CPUs of GPU dev's NUMA node, so host buffers
+    are first touched there; returns the node, or None if unknown."""
+    node = gpu_numa_node(torch, dev)
+    if node is None:
+        return None
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = set()
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus.update(range(int(lo), int(hi or lo) + 1))
+        allowed = os.sched_getaffinity(0) & cpus
+        if not allowed:
+            return None
+        os.sched_setaffinity(0, allowed)
+        return node
+    except (OSError, ValueError):
+        return None
+
+
+def main_one_process(args, devs, host_node=None):
     """N GPUs from ONE process (BASELINE config 5's shape, the way
     a Go process on the node drives them through the C-ABI): the blob is N
     parts of --size-gib GiB, part k resident in HBM on devs[k] (bytes = the
@@ -340,6 +381,7 @@ def main_one_process(args, devs):
                                   "(glfsx_create_devices)"},
         "devices": devs,
         "rehearsal": len(set(devs)) < nd,
+        "host_numa_node": host_node,
         "root_cid": bytes(root.ref)[:32].hex(),
         "per_device_ms": {"parts": [round(x, 3) for x in mean[:nd]],
                           "levels_above": round(mean[nd], 3) if len(mean) > nd else None,

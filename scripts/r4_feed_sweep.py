@@ -18,6 +18,9 @@ from glfs_amd import _native as N  # noqa: E402
 
 GIB, MIB = 1 << 30, 1 << 20
 bs, n = MIB, 4 * GIB
+bound = None
+if os.environ.get("FEED_NUMA") == "1":   # run on the GPU's NUMA node
+    bound = bench.numa_bind(torch, 0)
 host = bench.host_stream(torch, N, n, 3)
 root = N.glfsx_root()
 counts = (ctypes.c_uint64 * 2)()
@@ -30,7 +33,8 @@ for _ in range(3):
     dt = time.perf_counter() - t
     best = dt if best is None else min(best, dt)
 want = bytes(root.ref)
-res = {"env": {k: v for k, v in os.environ.items() if k.startswith("GLFSX_")},
+res = {"env": {k: v for k, v in os.environ.items() if k.startswith(("GLFSX_", "FEED_"))},
+       "numa_node": bound,
        "pageable_count_sink": round(n / GIB / best, 2)}
 res.update(bench.file_feed(N, host, bs, {"lanes_1": [0]}, want))
 res.pop("what", None)
