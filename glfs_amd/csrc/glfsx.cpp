@@ -168,7 +168,12 @@ int ctx_get(Ctx **out) {
 // At most kMaxSpinners threads poll at once (glfs.Machine is used
 // concurrently; N pollers would pin N host cores); the rest block at once,
 // and a poller yields its core between queries.
-constexpr int64_t kSpinNs = 2000000;
+// GLFSX_SPIN_US overrides the poll bound (A/B: config 4's 4.9 ms call waited
+// its last ~3 ms blocked at the 2 ms default)
+const int64_t kSpinNs = [] {
+  const char *e = getenv("GLFSX_SPIN_US");
+  return e ? int64_t(strtoll(e, nullptr, 10)) * 1000 : int64_t(2000000);
+}();
 constexpr int kMaxSpinners = 4;
 std::atomic<int> g_spinners{0};
 hipError_t stream_wait(hipStream_t s) {
