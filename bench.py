@@ -885,7 +885,7 @@ def config2_leg(torch, N, stream, sp, steps=50, warmup=5):
                     "salt, splitmix seed 1 in HBM, ctext to HBM; mean over steps (HIP events)"}
 
 
-def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
+def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10, routes=None):
     """BASELINE config 4 end to end: 1,048,576 distinct 4 KiB blobs (blob i =
     splitmix stream of seed i) posted as glfs blobs (DEK + ChaCha20 ctext to
     HBM + CID per blob, machine.go:64), then the tree of them ("%07d" names,
@@ -997,6 +997,8 @@ def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
     res = {}
     for name, fn in (("device", device_route_timed), ("one_call", one_call_route),
                      ("host", host_route)):
+        if routes is not None and name not in routes:
+            continue
         fn()
         ts, parts = [], []
         for _ in range(reps):
@@ -1023,6 +1025,8 @@ def config4_end_to_end(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
             res[name]["pieces_what"] = ("means of HIP events on the launch stream in the same "
                                         "reps; wall = gpu_ms + host_gaps_ms (launch and sync "
                                         "overheads between the pieces)")
+    if routes is not None:   # a subset for profiling (scripts/legs.py config4one)
+        return res
     assert res["device"]["tree_root_cid"] == res["host"]["tree_root_cid"]
     assert res["one_call"]["tree_root_cid"] == res["host"]["tree_root_cid"]
     out = dict(res["one_call"])

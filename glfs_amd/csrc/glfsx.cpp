@@ -2967,23 +2967,34 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   // B's tree posts come after everything already on A
   HIP_TRY(hipEventRecord(c->events[K], A));
   HIP_TRY(hipStreamWaitEvent(B, c->events[K], 0));
-  // the layout first, on A: beside the hashing it is starved (the small-blob
-  // passes hold every workgroup slot of the chip, and k_tree_prefix's
-  // 1024-thread workgroup gets a CU only when a pass drains: 0.49 ms instead
-  // of 9 us, with the host blocked behind it and a 0.15 ms hole on A)
-  HIP_TRY(launch_tree_layout(tj, A));
+  static const bool half = [] {  // GLFSX_TREE_HALF=0: full workgroups (A/B)
+    const char *e = getenv("GLFSX_TREE_HALF");
+    return !e || atoi(e) != 0;
+  }();
+  // GLFSX_TREE_BESIDE (default 1; 0 = the first round-4 order, A/B): the
+  // layout runs on B beside the blobs' DEK pass as well, its prefix in one
+  // 256-thread workgroup and every layout / static-line wave at raised issue
+  // priority.  Otherwise the layout runs first on A (a 1024-thread prefix
+  // beside the DEK pass waits for a CU until the pass drains) and the static
+  // lines, at the oldest-first SIMD's leftover issue, ended 74 us after the
+  // DEK pass (0.09 ms before the CID pass could start; profiles/r4/
+  // c4_timeline.txt).
+  static const bool beside_env = [] {
+    const char *e = getenv("GLFSX_TREE_BESIDE");
+    return !e || atoi(e) != 0;
+  }();
+  const bool beside = fuse && half && beside_env;
+  hipStream_t L = beside ? B : A;  // the layout's stream
+  tj.prio = beside ? 1u : 0u;
+  HIP_TRY(launch_tree_layout(tj, L));
   // exclusive prefix per entry workgroup, then the total (one copy)
-  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, A));
-  HIP_TRY(hipEventRecord(c->events[K + 1], A));
+  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, L));
+  HIP_TRY(hipEventRecord(c->events[K + 1], L));
   hipEvent_t static_done = nullptr;
   if (fuse) {
     // B: the lines without their hex digits, and where each root's digits go
     tj.hex_pos = tj.scratch + words;
-    HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
-    static const bool half = [] {  // GLFSX_TREE_HALF=0: full workgroups (A/B)
-      const char *e = getenv("GLFSX_TREE_HALF");
-      return !e || atoi(e) != 0;
-    }();
+    if (!beside) HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
     if (half)
       HIP_TRY(launch_tree_static(tj, B));
     else
@@ -3034,17 +3045,25 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
                 (unsigned long long)total, (unsigned long long)lines_cap);
   }
   const uint64_t nblk = (total + tree_bs - 1) / tree_bs;
+  // the tree blob's posts: with one group (the lines complete when A's CID
+  // pass ends) on A itself, after it -- no cross-stream event in the chain;
+  // with several groups on B, each group's blocks beside the next group
+  static const bool on_a_env = [] {  // GLFSX_TREE_ON_A=0: on B (A/B)
+    const char *e = getenv("GLFSX_TREE_ON_A");
+    return !e || atoi(e) != 0;
+  }();
+  const hipStream_t T = (fuse && on_a_env) ? A : B;
   if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
-                            tree_bs, B))
+                            tree_bs, T))
     return e;
   uint8_t *lvl = c->d_lvl_a.u8();
-  // on B: each tree block once all its bytes are written
+  // on T: each tree block once all its bytes are written
   uint64_t t_done = 0;
   for (uint64_t b = 0; b < K; ++b) {
     const uint64_t g1 = wgs * (b + 1) / K;
     const uint64_t ready = b + 1 == K ? total : prefix[g1];
     const uint64_t t_ready = b + 1 == K ? nblk : ready / tree_bs;
-    HIP_TRY(hipStreamWaitEvent(B, c->events[b], 0));
+    if (T != A) HIP_TRY(hipStreamWaitEvent(T, c->events[b], 0));
     if (t_ready > t_done) {
       PostJob j{};
       j.src = static_cast<const uint8_t *>(d_lines) + t_done * tree_bs;
@@ -3056,7 +3075,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
       j.out = RefLayout{lvl + 64 * t_done, ~0ull, 0};  // ref t at byte 64t
       words_from_key(j.salt, tsalts.raw);
       cid_words(j, cid_key);
-      HIP_TRY(launch_post(j, B, tls_fused));
+      HIP_TRY(launch_post(j, T, tls_fused));
       t_done = t_ready;
     }
   }
@@ -3065,15 +3084,20 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   tree_root->block_size = tree_bs;
   if (nblk <= 1) {  // one block: its ref is the root (blob.go:190-193)
     if (int e = c->h_root.ensure(64)) return e;
-    HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, B));
-    HIP_TRY(stream_wait(B));
-    if (int e = fused_check(B)) return e;
+    HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, T));
+    HIP_TRY(stream_wait(T));
+    if (T != B) HIP_TRY(stream_wait(B));
+    if (int e = fused_check(T)) return e;
     memcpy(tree_root->ref, c->h_root.p, 64);
     return 0;
   }
   uint64_t posts = 0;
-  return build_up(c, B, tsalts, cid_key, tree_bs, lvl, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
-                  &c->d_lvl_b, tree_root->ref, &posts);
+  if (int e = build_up(c, T, tsalts, cid_key, tree_bs, lvl,
+                       (nblk + tree_bs / 64 - 1) / (tree_bs / 64), &c->d_lvl_b,
+                       tree_root->ref, &posts))
+    return e;
+  if (T != B) HIP_TRY(stream_wait(B));  // (drained already: A waited for B's lines)
+  return 0;
 }
 }  // namespace
 

@@ -166,6 +166,9 @@ struct TreeJob {
   // first cid digit (its dek digits start kDekAfterCid bytes later); the
   // small-blob CID pass writes them (SmallJob::hex_out)
   uint64_t *hex_pos;
+  // nonzero: the layout and static-line kernels run beside the small-blob
+  // DEK pass (a 256-thread prefix, raised wave priority)
+  uint32_t prio;
 };
 // `<64 cid digits>","dek":"<64 dek digits>`: the dek's digits follow the
 // cid's first digit by 64 + len("\",\"dek\":\"") bytes

@@ -44,6 +44,7 @@ struct TArgs {
   uint64_t cap;         // bytes at out; nothing is written if the total exceeds it
   const uint64_t *total;
   uint64_t *hex_pos;    // nullable: skip the hex digits, record where they go
+  uint32_t prio;        // nonzero: the waves raise their issue priority
 };
 
 constexpr uint32_t kImg = 60 * 1024;  // LDS image per workgroup
@@ -286,6 +287,7 @@ __device__ uint32_t line(const TArgs &a, uint64_t i, S k, uint32_t *cid_at = nul
 
 __global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
   __shared__ uint64_t s[kTreeWG];
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   const uint64_t i = uint64_t(blockIdx.x) * kTreeWG + threadIdx.x;
   uint64_t v = i < a.n ? line(a, i, CountSink{}) : 0;
   s[threadIdx.x] = v;
@@ -301,18 +303,23 @@ __global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
   if (threadIdx.x == kTreeWG - 1) a.wg_total[blockIdx.x] = v;
 }
 
-// One workgroup: wg_total[0..m) -> exclusive prefix, in chunks of 1024.
-__global__ __launch_bounds__(1024) void k_tree_prefix(uint64_t *t, uint64_t m,
-                                                      uint64_t *total) {
-  __shared__ uint64_t s[1024];
+// One workgroup of T threads: wg_total[0..m) -> exclusive prefix, in chunks
+// of T.  T = 256 (one wave per SIMD) runs beside the small-blob DEK pass,
+// which leaves each SIMD room for one more wave; 1024 waits for a CU it
+// cannot get there.
+template <uint32_t T>
+__global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint64_t *total,
+                                                   uint32_t prio) {
+  __shared__ uint64_t s[T];
+  if (prio) __builtin_amdgcn_s_setprio(3);
   uint64_t carry = 0;
-  for (uint64_t c0 = 0; c0 < m; c0 += 1024) {
+  for (uint64_t c0 = 0; c0 < m; c0 += T) {
     const uint64_t i = c0 + threadIdx.x;
     const uint64_t x = i < m ? t[i] : 0;
     uint64_t v = x;
     s[threadIdx.x] = v;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
+    for (uint32_t d = 1; d < T; d <<= 1) {
       const uint64_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
       __syncthreads();
       v += add;
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(1024) void k_tree_prefix(uint64_t *t, uint64_t m,
       __syncthreads();
     }
     if (i < m) t[i] = carry + v - x;
-    carry += s[1023];
+    carry += s[T - 1];
     __syncthreads();
   }
   if (threadIdx.x == 0) *total = carry;
@@ -385,6 +392,9 @@ constexpr uint32_t kHalf = kTreeWG / 2;
 constexpr uint32_t kHalfImg = 30 * 1024;
 __global__ __launch_bounds__(kHalf) void k_tree_write_half(TArgs a) {
   __shared__ uint4 img4[kHalfImg / 16];
+  // beside the DEK pass: issue ahead of its resident waves (the SIMD issues
+  // oldest-first, so this youngest wave would otherwise take what is left)
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   uint8_t *img = reinterpret_cast<uint8_t *>(img4);
   const uint64_t wg = blockIdx.x >> 1, h = blockIdx.x & 1u;
   const uint64_t e0 = wg * kTreeWG + h * kHalf;  // this half's first entry
@@ -471,6 +481,7 @@ TArgs tree_args(const TreeJob &j) {
   a.cap = j.cap;
   a.total = j.total;
   a.hex_pos = j.hex_pos;
+  a.prio = j.prio;
   return a;
 }
 }  // namespace
@@ -482,7 +493,12 @@ hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s) {
   hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs, j.total);
+  if (j.prio)  // beside the DEK pass
+    hipLaunchKernelGGL(k_tree_prefix<256>, dim3(1), dim3(256), 0, s, a.wg_total, wgs, j.total,
+                       1u);
+  else
+    hipLaunchKernelGGL(k_tree_prefix<1024>, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
+                       j.total, 0u);
   return hipGetLastError();
 }
 
@@ -508,8 +524,8 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
   hipLaunchKernelGGL(k_tree_len, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tree_prefix, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
-                     j.total);
+  hipLaunchKernelGGL(k_tree_prefix<1024>, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
+                     j.total, 0u);
   e = hipGetLastError();
   if (e != hipSuccess || !j.out) return e;
   hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a, 0u);

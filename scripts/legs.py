@@ -2,7 +2,7 @@
 config 4's small-blob kernels (bench.small_blobs) and the read side
 (batched getF decrypt over a --gib GiB blob at 1 MiB blocks), and config 4
 end to end (bench.config4_end_to_end: blobs, tree lines, tree blob).
-usage: python scripts/legs.py [small|read|both|config4] [--gib G]"""
+usage: python scripts/legs.py [small|read|both|config4|config4one] [--gib G]"""
 import ctypes
 import json
 import os
@@ -38,6 +38,9 @@ def main():
         out["read_side"] = roof["read_side"]
     if what == "config4":
         out["config4_end_to_end"] = bench.config4_end_to_end(torch, N, stream, sp)
+    if what == "config4one":   # the one-call route alone, 20 reps
+        out["config4_one_call"] = bench.config4_end_to_end(torch, N, stream, sp, reps=20,
+                                                           routes=("one_call",))
     print(json.dumps(out), flush=True)
 
 
