@@ -2983,12 +2983,26 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     const char *e = getenv("GLFSX_TREE_BESIDE");
     return !e || atoi(e) != 0;
   }();
+  static const bool prio_env = [] {  // GLFSX_TREE_PRIO=0: no raised priority (A/B)
+    const char *e = getenv("GLFSX_TREE_PRIO");
+    return !e || atoi(e) != 0;
+  }();
   const bool beside = fuse && half && beside_env;
   hipStream_t L = beside ? B : A;  // the layout's stream
-  tj.prio = beside ? 1u : 0u;
-  HIP_TRY(launch_tree_layout(tj, L));
-  // exclusive prefix per entry workgroup, then the total (one copy)
-  HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost, L));
+  tj.prio = beside ? (prio_env ? 1u : 2u) : 0u;
+  if (beside) {
+    // one group needs only the total: the prefix kernel stores it in the
+    // pinned word the host reads (a copy kernel behind it on B would wait
+    // for a CU beside the DEK pass -- 1.1 ms in the trace -- and the static
+    // lines behind the copy)
+    tj.total_host = reinterpret_cast<uint64_t *>(c->h_tree.dptr()) + wgs;
+    HIP_TRY(launch_tree_layout(tj, L));
+  } else {
+    HIP_TRY(launch_tree_layout(tj, L));
+    // exclusive prefix per entry workgroup, then the total (one copy)
+    HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost,
+                           L));
+  }
   HIP_TRY(hipEventRecord(c->events[K + 1], L));
   hipEvent_t static_done = nullptr;
   if (fuse) {

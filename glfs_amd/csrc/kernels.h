@@ -167,8 +167,11 @@ struct TreeJob {
   // small-blob CID pass writes them (SmallJob::hex_out)
   uint64_t *hex_pos;
   // nonzero: the layout and static-line kernels run beside the small-blob
-  // DEK pass (a 256-thread prefix, raised wave priority)
+  // DEK pass (a 256-thread prefix; 1: also at raised wave priority)
   uint32_t prio;
+  // nullable, pinned host memory (device pointer): the layout's prefix
+  // kernel also stores the total there (no copy behind it on the stream)
+  uint64_t *total_host;
 };
 // `<64 cid digits>","dek":"<64 dek digits>`: the dek's digits follow the
 // cid's first digit by 64 + len("\",\"dek\":\"") bytes

@@ -287,7 +287,7 @@ __device__ uint32_t line(const TArgs &a, uint64_t i, S k, uint32_t *cid_at = nul
 
 __global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
   __shared__ uint64_t s[kTreeWG];
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(3);
   const uint64_t i = uint64_t(blockIdx.x) * kTreeWG + threadIdx.x;
   uint64_t v = i < a.n ? line(a, i, CountSink{}) : 0;
   s[threadIdx.x] = v;
@@ -309,9 +309,9 @@ __global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
 // cannot get there.
 template <uint32_t T>
 __global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint64_t *total,
-                                                   uint32_t prio) {
+                                                   uint32_t prio, uint64_t *total_host) {
   __shared__ uint64_t s[T];
-  if (prio) __builtin_amdgcn_s_setprio(3);
+  if (prio == 1) __builtin_amdgcn_s_setprio(3);
   uint64_t carry = 0;
   for (uint64_t c0 = 0; c0 < m; c0 += T) {
     const uint64_t i = c0 + threadIdx.x;
@@ -330,7 +330,12 @@ __global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint
     carry += s[T - 1];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *total = carry;
+  if (threadIdx.x == 0) {
+    *total = carry;
+    // the host's copy (pinned), read once the launch's event completes
+    if (total_host) __hip_atomic_store(total_host, carry, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // wg0: the first entry workgroup of this launch (a range of them is written
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(kHalf) void k_tree_write_half(TArgs a) {
   __shared__ uint4 img4[kHalfImg / 16];
   // beside the DEK pass: issue ahead of its resident waves (the SIMD issues
   // oldest-first, so this youngest wave would otherwise take what is left)
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(3);
   uint8_t *img = reinterpret_cast<uint8_t *>(img4);
   const uint64_t wg = blockIdx.x >> 1, h = blockIdx.x & 1u;
   const uint64_t e0 = wg * kTreeWG + h * kHalf;  // this half's first entry
@@ -495,10 +500,10 @@ hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s) {
   if (e != hipSuccess) return e;
   if (j.prio)  // beside the DEK pass
     hipLaunchKernelGGL(k_tree_prefix<256>, dim3(1), dim3(256), 0, s, a.wg_total, wgs, j.total,
-                       1u);
+                       j.prio, j.total_host);
   else
     hipLaunchKernelGGL(k_tree_prefix<1024>, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
-                       j.total, 0u);
+                       j.total, 0u, j.total_host);
   return hipGetLastError();
 }
 
@@ -525,7 +530,7 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tree_prefix<1024>, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
-                     j.total, 0u);
+                     j.total, 0u, static_cast<uint64_t *>(nullptr));
   e = hipGetLastError();
   if (e != hipSuccess || !j.out) return e;
   hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a, 0u);
