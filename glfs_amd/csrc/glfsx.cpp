@@ -2988,6 +2988,34 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     return !e || atoi(e) != 0;
   }();
   const bool beside = fuse && half && beside_env;
+  SmallJob sj{};
+  sj.src = static_cast<const uint8_t *>(d_data);
+  sj.ctext = static_cast<uint8_t *>(d_ctext);
+  sj.max_len = max_len;
+  sj.small_max = small_max_for(blob_bs);
+  words_from_key(sj.raw_salt, bsalts.raw);
+  words_from_key(sj.index_salt, bsalts.index);
+  if (cid_key) {
+    words_from_key(sj.cid_key, cid_key);
+    sj.cid_keyed = true;
+  } else {
+    blake3_iv_words(sj.cid_key);
+  }
+  static const bool dek_first_env = [] {  // GLFSX_DEK_FIRST=0: the layout first (A/B)
+    const char *e = getenv("GLFSX_DEK_FIRST");
+    return !e || atoi(e) != 0;
+  }();
+  const bool dek_first = beside && dek_first_env;
+  if (dek_first) {
+    // the blobs' DEK pass (the critical path) queued first; the layout and
+    // static lines follow on B beside it, then the CID pass below
+    sj.offs = d_offsets;
+    sj.lens = d_lengths;
+    sj.n = n;
+    sj.refs = static_cast<uint8_t *>(d_roots);
+    sj.passes = 1;
+    HIP_TRY(launch_post_small(sj, A));
+  }
   hipStream_t L = beside ? B : A;  // the layout's stream
   tj.prio = beside ? (prio_env ? 1u : 2u) : 0u;
   if (beside) {
@@ -3016,19 +3044,6 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     static_done = c->events[K + 2];
     HIP_TRY(hipEventRecord(static_done, B));
   }
-  SmallJob sj{};
-  sj.src = static_cast<const uint8_t *>(d_data);
-  sj.ctext = static_cast<uint8_t *>(d_ctext);
-  sj.max_len = max_len;
-  sj.small_max = small_max_for(blob_bs);
-  words_from_key(sj.raw_salt, bsalts.raw);
-  words_from_key(sj.index_salt, bsalts.index);
-  if (cid_key) {
-    words_from_key(sj.cid_key, cid_key);
-    sj.cid_keyed = true;
-  } else {
-    blake3_iv_words(sj.cid_key);
-  }
   // every group's hashing and lines queued on A before the host waits for
   // the layout (k_tree_write skips its work when the lines exceed the cap)
   for (uint64_t b = 0; b < K; ++b) {
@@ -3042,6 +3057,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
       sj.hex_out = static_cast<uint8_t *>(d_lines);
       sj.hex_pos = tj.hex_pos;
       sj.cid_wait = static_done;
+      sj.passes = dek_first ? 2u : 0u;  // (the DEK pass may be queued already)
       HIP_TRY(launch_post_small(sj, A));
     } else {
       HIP_TRY(launch_post_small(sj, A));

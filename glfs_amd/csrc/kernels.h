@@ -88,6 +88,7 @@ struct SmallJob {
   uint8_t *hex_out;
   const uint64_t *hex_pos;
   hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
+  uint32_t passes;      // 1: the DEK pass only, 2: the CID pass only, 0: both
 };
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }

@@ -3073,8 +3073,11 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   }
   a.base = kKeyed;
   a.out_off = 32;
-  hipError_t e = launch_small_pass<false>(a, max_len, s);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (job.passes != 2) {
+    e = launch_small_pass<false>(a, max_len, s);
+    if (e != hipSuccess || job.passes == 1) return e;
+  }
   for (int i = 0; i < 8; ++i) a.key[i] = a.key0[i] = job.cid_key[i];
   a.base = job.cid_keyed ? kKeyed : 0u;
   a.out_off = 0;

@@ -1,7 +1,8 @@
 """Config-4 one-call timeline from a rocprofv3 kernel (+ memory copy) trace of
 `scripts/legs.py config4one`: every kernel and copy of one call, both
-streams, as start / end offsets from the call's first kernel (k_tree_len, the
-layout), plus the mean span over the calls (warm-up calls skipped).
+streams, as start / end offsets from the call's first kernel (the blobs'
+DEK pass, or k_tree_len where the layout goes first), plus the mean span
+over the calls (warm-up calls skipped).
 
 usage: python scripts/c4_timeline.py <trace dir> [skip]"""
 import csv
@@ -31,11 +32,16 @@ def main(d, skip=2):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                    "copy " + r.get("Direction", "?"), "copy"))
     ev.sort()
+    # a call starts with its blobs' DEK pass when that is queued first (the
+    # default order), else with the layout
+    names = [e[2] for e in ev]
+    first = next((k for k in names if k.startswith("k_small_q<4, false") or k == "k_tree_len"),
+                 "k_tree_len")
     calls, cur = [], None
     for e in ev:
         if e[2].startswith("k_fill"):
             continue
-        if e[2] == "k_tree_len":
+        if e[2] == first:
             cur = []
             calls.append(cur)
         if cur is not None:
