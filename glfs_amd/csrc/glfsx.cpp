@@ -3023,7 +3023,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     // pinned word the host reads (a copy kernel behind it on B would wait
     // for a CU beside the DEK pass -- 1.1 ms in the trace -- and the static
     // lines behind the copy)
-    tj.total_host = reinterpret_cast<uint64_t *>(c->h_tree.dptr()) + wgs;
+    tj.prefix_host = reinterpret_cast<uint64_t *>(c->h_tree.dptr());
     HIP_TRY(launch_tree_layout(tj, L));
   } else {
     HIP_TRY(launch_tree_layout(tj, L));
@@ -3044,9 +3044,47 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     static_done = c->events[K + 2];
     HIP_TRY(hipEventRecord(static_done, B));
   }
+  // GLFSX_TREE_SPLIT=P (1-99; default 0 = off, measured slower): with the
+  // layout beside, the CID pass runs as two launches, the first P % of the
+  // entry workgroups, then the rest on 3/4 of the chip; the tree blocks
+  // whose lines are complete after the first (their bytes end before the
+  // first entry of the second) are posted on B beside the second, and only
+  // the last few blocks -- a split plan of short lanes -- and the index node
+  // remain after it.  In the trace the tree blocks' DEK pass on B got almost
+  // no CU time beside the second group (571 us instead of 105) and the
+  // second group ran slower on 3/4 of the chip: config 4 820 / 823 GiB/s at
+  // P = 85 / 70 vs 836 unsplit.
+  static const uint64_t split_env = [] {
+    const char *e = getenv("GLFSX_TREE_SPLIT");
+    return e ? strtoull(e, nullptr, 10) : 0ull;
+  }();
+  const uint64_t g_split = (beside && dek_first && split_env > 0 && split_env < 100 && wgs >= 8)
+                               ? std::max<uint64_t>(1, wgs * split_env / 100) : 0;
+  if (g_split) {
+    const uint64_t e1 = g_split * kTreeWG;
+    sj.hex_out = static_cast<uint8_t *>(d_lines);
+    sj.hex_pos = tj.hex_pos;
+    sj.passes = 2;
+    sj.offs = d_offsets;
+    sj.lens = d_lengths;
+    sj.n = e1;
+    sj.refs = static_cast<uint8_t *>(d_roots);
+    sj.cid_wait = static_done;
+    HIP_TRY(launch_post_small(sj, A));
+    HIP_TRY(hipEventRecord(c->events[K + 3], A));  // the first group's lines are done
+    sj.offs = d_offsets + e1;
+    sj.lens = d_lengths + e1;
+    sj.n = n - e1;
+    sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e1;
+    sj.hex_pos = tj.hex_pos + e1;  // indexed by the group's own blob numbers
+    sj.cid_wait = nullptr;
+    sj.quarters = 3;
+    HIP_TRY(launch_post_small(sj, A));
+    HIP_TRY(hipEventRecord(c->events[0], A));
+  }
   // every group's hashing and lines queued on A before the host waits for
   // the layout (k_tree_write skips its work when the lines exceed the cap)
-  for (uint64_t b = 0; b < K; ++b) {
+  for (uint64_t b = 0; b < K && !g_split; ++b) {
     const uint64_t g0 = wgs * b / K, g1 = wgs * (b + 1) / K;
     const uint64_t e0 = g0 * kTreeWG, e1 = std::min(n, g1 * kTreeWG);
     sj.offs = d_offsets + e0;
@@ -3083,29 +3121,46 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     return !e || atoi(e) != 0;
   }();
   const hipStream_t T = (fuse && on_a_env) ? A : B;
+  // split CID pass: the blocks complete after its first group go on B
+  const uint64_t t_split = g_split ? std::min(prefix[g_split] / tree_bs, nblk) : 0;
+  hipStream_t P = t_split ? B : T;  // the level buffer's preparation
+  if (t_split) HIP_TRY(hipStreamWaitEvent(B, c->events[K + 3], 0));
   if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
-                            tree_bs, T))
+                            tree_bs, P))
     return e;
   uint8_t *lvl = c->d_lvl_a.u8();
+  auto post_tree_blocks = [&](uint64_t t0, uint64_t t1, hipStream_t s) -> int {
+    PostJob j{};
+    j.src = static_cast<const uint8_t *>(d_lines) + t0 * tree_bs;
+    j.ctext = d_tree_ctext ? static_cast<uint8_t *>(d_tree_ctext) + t0 * tree_bs : nullptr;
+    j.stride = tree_bs;
+    j.msg_len = tree_bs;
+    j.n = t1 - t0;
+    j.last_len = t1 == nblk ? total - (nblk - 1) * tree_bs : tree_bs;
+    j.out = RefLayout{lvl + 64 * t0, ~0ull, 0};  // ref t at byte 64t
+    words_from_key(j.salt, tsalts.raw);
+    cid_words(j, cid_key);
+    HIP_TRY(launch_post(j, s, tls_fused));
+    return 0;
+  };
+  if (g_split) {
+    if (t_split) {
+      if (int e = post_tree_blocks(0, t_split, B)) return e;
+      HIP_TRY(hipEventRecord(c->events[K + 3], B));
+    }
+    if (t_split < nblk)  // on A after the second group (few blocks: short lanes)
+      if (int e = post_tree_blocks(t_split, nblk, A)) return e;
+    if (t_split) HIP_TRY(hipStreamWaitEvent(A, c->events[K + 3], 0));
+  }
   // on T: each tree block once all its bytes are written
   uint64_t t_done = 0;
-  for (uint64_t b = 0; b < K; ++b) {
+  for (uint64_t b = 0; b < K && !g_split; ++b) {
     const uint64_t g1 = wgs * (b + 1) / K;
     const uint64_t ready = b + 1 == K ? total : prefix[g1];
     const uint64_t t_ready = b + 1 == K ? nblk : ready / tree_bs;
     if (T != A) HIP_TRY(hipStreamWaitEvent(T, c->events[b], 0));
     if (t_ready > t_done) {
-      PostJob j{};
-      j.src = static_cast<const uint8_t *>(d_lines) + t_done * tree_bs;
-      j.ctext = d_tree_ctext ? static_cast<uint8_t *>(d_tree_ctext) + t_done * tree_bs : nullptr;
-      j.stride = tree_bs;
-      j.msg_len = tree_bs;
-      j.n = t_ready - t_done;
-      j.last_len = t_ready == nblk ? total - (nblk - 1) * tree_bs : tree_bs;
-      j.out = RefLayout{lvl + 64 * t_done, ~0ull, 0};  // ref t at byte 64t
-      words_from_key(j.salt, tsalts.raw);
-      cid_words(j, cid_key);
-      HIP_TRY(launch_post(j, T, tls_fused));
+      if (int e = post_tree_blocks(t_done, t_ready, T)) return e;
       t_done = t_ready;
     }
   }
@@ -3118,6 +3173,8 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     HIP_TRY(stream_wait(T));
     if (T != B) HIP_TRY(stream_wait(B));
     if (int e = fused_check(T)) return e;
+    if (T != B)
+      if (int e = fused_check(B)) return e;
     memcpy(tree_root->ref, c->h_root.p, 64);
     return 0;
   }
@@ -3126,7 +3183,10 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
                        (nblk + tree_bs / 64 - 1) / (tree_bs / 64), &c->d_lvl_b,
                        tree_root->ref, &posts))
     return e;
-  if (T != B) HIP_TRY(stream_wait(B));  // (drained already: A waited for B's lines)
+  if (T != B) {
+    HIP_TRY(stream_wait(B));  // (drained already: A waited for B's work)
+    if (int e = fused_check(B)) return e;  // tree posts on B (split CID pass)
+  }
   return 0;
 }
 }  // namespace

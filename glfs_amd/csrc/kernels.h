@@ -89,6 +89,8 @@ struct SmallJob {
   const uint64_t *hex_pos;
   hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
   uint32_t passes;      // 1: the DEK pass only, 2: the CID pass only, 0: both
+  uint32_t quarters;    // k_small_q's grid: this many quarters of what the
+                        // chip holds (0: all), leaving room for other work
 };
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
@@ -170,9 +172,10 @@ struct TreeJob {
   // nonzero: the layout and static-line kernels run beside the small-blob
   // DEK pass (a 256-thread prefix; 1: also at raised wave priority)
   uint32_t prio;
-  // nullable, pinned host memory (device pointer): the layout's prefix
-  // kernel also stores the total there (no copy behind it on the stream)
-  uint64_t *total_host;
+  // nullable, pinned host memory (device pointer) of ceil(n / 256) + 1
+  // words: the layout's prefix kernel also stores the per-workgroup
+  // exclusive prefix and then the total there (no copy kernel behind it)
+  uint64_t *prefix_host;
 };
 // `<64 cid digits>","dek":"<64 dek digits>`: the dek's digits follow the
 // cid's first digit by 64 + len("\",\"dek\":\"") bytes

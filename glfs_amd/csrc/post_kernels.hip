@@ -2762,8 +2762,9 @@ uint32_t small_fine_div() {
 }
 
 template <int G, bool CHACHA, int A>
-hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
-  static const uint32_t slots = resident_wgs(k_small_q<G, CHACHA, A>);
+hipError_t launch_small_q(const SArgs &a0, hipStream_t s, uint32_t quarters) {
+  static const uint32_t all = resident_wgs(k_small_q<G, CHACHA, A>);
+  const uint32_t slots = (quarters && all) ? std::max(1u, all / 4 * quarters) : all;
   uint32_t *ctr;
   uint32_t epoch;
   hipError_t e = small_q_get(s, &ctr, &epoch);
@@ -2781,7 +2782,8 @@ hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
 }
 
 template <bool CHACHA>
-hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
+hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s,
+                             uint32_t quarters = 0) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
   const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
   const int gsel = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0;
@@ -2800,11 +2802,11 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   constexpr int F = CHACHA ? GLFSX_SMALL_CID : GLFSX_SMALL_DEK;
   if (small_q_enabled()) {  // more workgroups than the chip holds: per-wave items
     switch (gsel) {
-      case 1: return launch_small_q<1, CHACHA, F>(a, s);
-      case 2: return launch_small_q<2, CHACHA, F>(a, s);
-      case 4: return launch_small_q<4, CHACHA, F>(a, s);
-      case 8: return launch_small_q<8, CHACHA, F>(a, s);
-      case 16: return launch_small_q<16, CHACHA, F>(a, s);
+      case 1: return launch_small_q<1, CHACHA, F>(a, s, quarters);
+      case 2: return launch_small_q<2, CHACHA, F>(a, s, quarters);
+      case 4: return launch_small_q<4, CHACHA, F>(a, s, quarters);
+      case 8: return launch_small_q<8, CHACHA, F>(a, s, quarters);
+      case 16: return launch_small_q<16, CHACHA, F>(a, s, quarters);
       default: return hipErrorInvalidValue;
     }
   }
@@ -3087,7 +3089,7 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
     e = hipStreamWaitEvent(s, job.cid_wait, 0);
     if (e != hipSuccess) return e;
   }
-  return launch_small_pass<true>(a, max_len, s);
+  return launch_small_pass<true>(a, max_len, s, job.quarters);
 }
 
 #if GLFSX_WGTIME

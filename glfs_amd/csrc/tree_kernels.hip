@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kTreeWG) void k_tree_len(TArgs a) {
 // cannot get there.
 template <uint32_t T>
 __global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint64_t *total,
-                                                   uint32_t prio, uint64_t *total_host) {
+                                                   uint32_t prio, uint64_t *host_out) {
   __shared__ uint64_t s[T];
   if (prio == 1) __builtin_amdgcn_s_setprio(3);
   uint64_t carry = 0;
@@ -326,15 +326,19 @@ __global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint
       s[threadIdx.x] = v;
       __syncthreads();
     }
-    if (i < m) t[i] = carry + v - x;
+    if (i < m) {
+      t[i] = carry + v - x;
+      // the host's copy (pinned), read once the launch's event completes
+      if (host_out) __hip_atomic_store(host_out + i, carry + v - x, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     carry += s[T - 1];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     *total = carry;
-    // the host's copy (pinned), read once the launch's event completes
-    if (total_host) __hip_atomic_store(total_host, carry, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+    if (host_out) __hip_atomic_store(host_out + m, carry, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -500,10 +504,10 @@ hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s) {
   if (e != hipSuccess) return e;
   if (j.prio)  // beside the DEK pass
     hipLaunchKernelGGL(k_tree_prefix<256>, dim3(1), dim3(256), 0, s, a.wg_total, wgs, j.total,
-                       j.prio, j.total_host);
+                       j.prio, j.prefix_host);
   else
     hipLaunchKernelGGL(k_tree_prefix<1024>, dim3(1), dim3(1024), 0, s, a.wg_total, wgs,
-                       j.total, 0u, j.total_host);
+                       j.total, 0u, j.prefix_host);
   return hipGetLastError();
 }
 

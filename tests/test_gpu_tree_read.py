@@ -427,7 +427,10 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
 
 
 @pytest.mark.parametrize("n,tree_bs", [(70_000, 2 * MIB), (3000, 4096), (300, 64 * 1024),
-                                       (1, 2 * MIB), (257, 1024)])
+                                       (1, 2 * MIB), (257, 1024),
+                                       # the CID pass in two groups with
+                                       # no / some tree blocks beside the second
+                                       (20_000, 8 * MIB), (20_000, MIB)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
     """glfsx_post_tree_device (blob hashing, tree lines and the tree blob
     overlapped) against the three calls in sequence on the same inputs:
