@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-4 check 18: the whole -m gpu suite, smoke(), and the default bench line
+# The round-end check on a GPU box: the whole -m gpu suite, smoke(), and the
+# default bench line (gpurun_out/r4_t18.log, r4_s18.log, r4_b18.json)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
