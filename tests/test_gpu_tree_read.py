@@ -502,3 +502,79 @@ def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
                                              dbs.data_ptr(), tree_bs, out2.data_ptr(),
                                              t1.value - 1, None, ctypes.byref(r2),
                                              ctypes.byref(t2), None))
+
+
+def test_post_tree_device_keyed_cid_and_ctext(gpu, O):
+    """The one call with a keyed CID and both ctext outputs (the blobs' and
+    the tree blob's) against the three calls with the same key, after a
+    call that failed on a short line buffer (the next call starts clean):
+    roots, lines, every ctext byte and the tree root."""
+    import ctypes
+    import random
+    import torch
+    from glfs_amd import _native as N
+    n, tree_bs = 5000, 64 * 1024
+    rng = random.Random(77)
+    lens_h = [rng.choice([0, 1, 100, 4096, 9000, 16384]) for _ in range(n)]
+    offs_h, o = [], 0
+    for ln in lens_h:
+        offs_h.append(o)
+        o += (ln + 15) // 16 * 16
+    data = torch.empty(o + 64, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), 0, o + 8 - o % 8, 3, None))
+    names = [b"k%05d" % i for i in range(n)]
+    types = [b"blob"] * n
+    modes = [0o644] * n
+    bss = [2 * MIB] * n
+    offs = torch.tensor(offs_h, dtype=torch.int64, device="cuda")
+    lens = torch.tensor(lens_h, dtype=torch.int64, device="cuda")
+    dn, dno, dm, dt, dto, _, dbs = _tree_inputs(torch, names, types, modes, lens_h, bss)
+    bsalt, tsalt = O.derive_key(bytes(32), b"blob"), O.derive_key(bytes(32), b"tree")
+    key = bytes(range(40, 72))
+    cap = 300 * n + 4096
+    torch.cuda.synchronize()
+    ct1 = torch.zeros(o + 64, dtype=torch.uint8, device="cuda")
+    roots1 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_post_blobs_device(2 * MIB, bsalt, key, data.data_ptr(), offs.data_ptr(),
+                                          lens.data_ptr(), n, 16384, ct1.data_ptr(),
+                                          roots1.data_ptr(), None))
+    out1 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    t1 = ctypes.c_uint64()
+    N.check(N.lib.glfsx_tree_encode_device(n, dn.data_ptr(), dno.data_ptr(), dm.data_ptr(),
+                                           dt.data_ptr(), dto.data_ptr(), roots1.data_ptr(),
+                                           lens.data_ptr(), dbs.data_ptr(), out1.data_ptr(),
+                                           cap, None, ctypes.byref(t1), None))
+    tct1 = torch.zeros(t1.value + 64, dtype=torch.uint8, device="cuda")
+    r1 = N.glfsx_root()
+    N.check(N.lib.glfsx_create_device(tree_bs, tsalt, key, out1.data_ptr(), t1.value,
+                                      tct1.data_ptr(), ctypes.byref(r1), None, None))
+    torch.cuda.synchronize()
+    ct2 = torch.zeros(o + 64, dtype=torch.uint8, device="cuda")
+    roots2 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    out2 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    tct2 = torch.zeros(t1.value + 64, dtype=torch.uint8, device="cuda")
+    r2, t2 = N.glfsx_root(), ctypes.c_uint64()
+
+    def one_call(cap2):
+        return N.lib.glfsx_post_tree_device(n, 2 * MIB, bsalt, tsalt, key, data.data_ptr(),
+                                            offs.data_ptr(), lens.data_ptr(), 16384,
+                                            ct2.data_ptr(), roots2.data_ptr(), dn.data_ptr(),
+                                            dno.data_ptr(), dm.data_ptr(), dt.data_ptr(),
+                                            dto.data_ptr(), dbs.data_ptr(), tree_bs,
+                                            out2.data_ptr(), cap2, tct2.data_ptr(),
+                                            ctypes.byref(r2), ctypes.byref(t2), None)
+    with pytest.raises(N.GlfsxError):
+        N.check(one_call(t1.value - 1))
+    N.check(one_call(cap))
+    torch.cuda.synchronize()
+    assert t2.value == t1.value
+    assert torch.equal(roots1, roots2)
+    assert torch.equal(out1[:t1.value], out2[:t2.value])
+    assert torch.equal(ct1[:o], ct2[:o])
+    assert torch.equal(tct1[:t1.value], tct2[:t1.value])
+    assert bytes(r2.ref) == bytes(r1.ref)
+    i = 4321
+    want_root, _, _, _ = O.create(bytes(data[offs_h[i]:offs_h[i] + lens_h[i]].cpu().numpy()
+                                        .tobytes()), 2 * MIB, salt=bsalt, cid_key=key,
+                                  closed_form=True)
+    assert bytes(roots2[64 * i:64 * i + 64].cpu().numpy().tobytes()) == want_root
