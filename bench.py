@@ -176,12 +176,16 @@ def main():
         step()
     barrier()
     torch.cuda.synchronize()
+    N.check(N.lib.glfsx_clock_probe(1, None))   # (synchronous; before the clock starts)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    probe = (ctypes.c_uint64 * 2)()
+    N.check(N.lib.glfsx_clock_probe(0, probe))
+    step_clock = round(probe[0] / probe[1] * 0.1, 3) if probe[1] else None
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -209,6 +213,10 @@ def main():
                    "parallelism": f"disjoint block ranges x{world}"},
         "root_cid": root_ref[0][:32].hex() if rank == 0 else None,
         "host_numa_node": host_node,
+        "held_clock_GHz": step_clock,
+        "held_clock_what": "shader clock over the timed steps' hashing launches on this "
+                           "rank's GPU (s_memtime cycles / s_memrealtime ticks summed over "
+                           "every k_pass workgroup, glfsx_clock_probe); peak 2.4",
     }
 
     if not args.no_extras:
@@ -529,20 +537,35 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
     salt = bytes(32)
     ct = None if ctext is None else ctext.data_ptr()
     times = {"dek": [], "cid": []}
+    # the clock the chip held over these very launches: every k_pass
+    # workgroup adds its lifetime in shader-clock cycles and in 100 MHz ticks
+    # to two device counters (glfsx_clock_probe), read after each timed pass
+    probe = (ctypes.c_uint64 * 2)()
+    clk = {"dek": [0, 0], "cid": [0, 0]}
+    N.check(N.lib.glfsx_clock_probe(1, None))
     with torch.cuda.stream(stream):
-        for _ in range(reps + 1):
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        for rep in range(reps + 1):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             e[0].record(stream)
             N.check(N.lib.glfsx_dek_batch_device(salt, data.data_ptr(), per, bs,
                                                  refs.data_ptr(), sp))
             e[1].record(stream)
+            e[1].synchronize()
+            N.check(N.lib.glfsx_clock_probe(1, probe))
+            if rep:   # the first rep is the warm-up
+                clk["dek"] = [clk["dek"][0] + probe[0], clk["dek"][1] + probe[1]]
+            e[2].record(stream)
             N.check(N.lib.glfsx_cid_batch_device(data.data_ptr(), per, bs, ct,
                                                  refs.data_ptr(), None, sp))
-            e[2].record(stream)
-            e[2].synchronize()
+            e[3].record(stream)
+            e[3].synchronize()
+            N.check(N.lib.glfsx_clock_probe(1, probe))
+            if rep:
+                clk["cid"] = [clk["cid"][0] + probe[0], clk["cid"][1] + probe[1]]
             times["dek"].append(e[0].elapsed_time(e[1]))
-            times["cid"].append(e[1].elapsed_time(e[2]))
+            times["cid"].append(e[2].elapsed_time(e[3]))
     avg = {k: sum(v[1:]) / reps for k, v in times.items()}  # first rep = warm-up
+    clock = {k: v[0] / v[1] * 0.1 for k, v in clk.items() if v[1]}   # GHz
     read = None
     if ct is not None:
         # read side (getF decrypt, ref.go:113-126): ctext -> ptext written over
@@ -568,7 +591,7 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
     kern_bytes = {"dek": per, "cid": per * (2 if ct is not None else 1)}
     dom = max(avg, key=avg.get)
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9
-    traffic, clock = None, {}
+    traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
@@ -576,7 +599,6 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
             t = pm.get(dom, {})
             # profiled at the 64 GiB launch; traffic is linear in blocks
             traffic = int(t["hbm_bytes_per_launch"] * kern_bytes[dom] / t["algorithmic_bytes"])
-            clock = pm.get("clock_GHz", {})
         except Exception:
             traffic = None
     ms_step = step_ms if step_ms else None
@@ -605,8 +627,10 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
             "held_clock_GHz": {k: round(v, 3) for k, v in clock.items()},
             "frac_at_held_clock": {k: round(ideal_ms[k] * PEAK_GHZ / clock[k] / avg[k], 3)
                                    for k in avg if k in clock},
-            "held_clock_source": "GRBM_GUI_ACTIVE / 8 / duration, rocprofv3 PMC pass of the "
-                                 "same launches (profiles/pmc_traffic.json)",
+            "held_clock_source": "this run: the timed launches themselves (every k_pass "
+                                 "workgroup sums its lifetime in s_memtime shader-clock "
+                                 "cycles and s_memrealtime 100 MHz ticks, glfsx_clock_probe; "
+                                 "GHz = cycles / ticks x 0.1), same reps as achieved_ms",
             "instr_per_byte": INSTR_PER_BYTE}
     del refs
     roof["read_side"] = read

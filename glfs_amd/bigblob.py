@@ -266,9 +266,21 @@ class Writer:
 
 
 def _regular_fd(r) -> Optional[int]:
-    """The descriptor of a seekable regular file behind r, or None."""
+    """The descriptor of a seekable regular file behind r, or None.
+
+    Only a plain file object qualifies: an io.FileIO, or a buffered reader
+    whose raw stream is one (what open(p, "rb") returns), so that tell() is
+    a byte offset into the descriptor's file.  A wrapper that transforms
+    the bytes (gzip / bz2 / lzma files, whose fileno() is the compressed
+    file's and whose tell() is a decompressed position) reads through
+    readinto instead."""
+    raw = r
+    if isinstance(r, (io.BufferedReader, io.BufferedRandom)):
+        raw = r.raw
+    if type(raw) is not io.FileIO:
+        return None
     try:
-        if not (hasattr(r, "fileno") and hasattr(r, "tell") and r.seekable()):
+        if not r.seekable():
             return None
         fd = r.fileno()
         return fd if stat.S_ISREG(os.fstat(fd).st_mode) else None

@@ -247,15 +247,6 @@ hipStream_t pick_stream(Ctx *c, void *stream) {
 // leadership.  Up to kOneLanes launches are in flight, each carrying
 // whatever queued while the earlier ones ran.  Per-caller launches would cap
 // the process at GPU_MAX_HW_QUEUES (4) posts in flight.
-// GLFSX_ONE=0 routes one-shot posts through the general passes (A/B runs).
-bool one_enabled() {
-  static const bool on = [] {
-    const char *e = getenv("GLFSX_ONE");
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
-
 constexpr uint32_t kOneBatch = 1024;
 constexpr int kOneLanes = 4;
 struct OneReq {
@@ -939,26 +930,22 @@ struct CopyPool {
     }
   }
 };
-// The CPUs of the NUMA node the current device hangs off (sysfs of its PCI
-// function), within this process's affinity; false if unknown.  The copy
-// pool's threads run there (GLFSX_NUMA=0: anywhere): their copies and reads
-// land in pinned staging the device's DMA engines read, and a file read
-// from the device's node ran 27-29 -> 35-38 GiB/s on a two-socket box
-// (bench file_feed).
-bool device_node_cpus(cpu_set_t *set) {
-  const char *e = getenv("GLFSX_NUMA");
-  if (e && atoi(e) == 0) return false;
-  int dev = 0;
+// The NUMA node device `dev` hangs off (sysfs of its PCI function), or -1.
+int device_numa_node(int dev) {
   char bdf[64] = {0};
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetPCIBusId(bdf, int(sizeof bdf) - 1, dev) != hipSuccess)
-    return false;
+  if (hipDeviceGetPCIBusId(bdf, int(sizeof bdf) - 1, dev) != hipSuccess) return -1;
   for (char *q = bdf; *q; ++q) *q = char(tolower(*q));
   int node = -1;
   if (FILE *f = fopen((std::string("/sys/bus/pci/devices/") + bdf + "/numa_node").c_str(), "r")) {
     if (fscanf(f, "%d", &node) != 1) node = -1;
     fclose(f);
   }
+  return node;
+}
+
+// The CPUs of NUMA node `node` within this process's affinity; false if
+// unknown or none.
+bool node_cpus(int node, cpu_set_t *set) {
   if (node < 0) return false;
   char path[96];
   snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
@@ -986,30 +973,60 @@ bool device_node_cpus(cpu_set_t *set) {
   return CPU_COUNT(set) > 0;
 }
 
-CopyPool &copy_pool() {
-  static CopyPool *p = [] {
-    auto *cp = new CopyPool();
-    const unsigned hw = std::thread::hardware_concurrency();
-    cp->workers = std::min(15u, hw > 1 ? hw - 1 : 0u);
-    cpu_set_t cpus;
-    const bool bind = device_node_cpus(&cpus);
-    for (unsigned i = 0; i < cp->workers; ++i)
-      std::thread([cp, bind, cpus] {
-        if (bind) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus, &cpus);
-        cp->run();
-      }).detach();
-    return cp;
+// One copy pool per NUMA node, used for the staging of a device on that
+// node: its threads run on the node's CPUs (GLFSX_NUMA=0: one unbound pool
+// for every device), so their copies and reads land in pinned staging the
+// device's DMA engines read -- a file read from the device's node ran 27-29
+// -> 35-38 GiB/s on a two-socket box (bench file_feed).
+// A process driving GPUs on both sockets (glfsx_create_devices, a Writer
+// over several lanes) gets a pool on each (one process-wide pool
+// bound to the first device's node served the other socket's GPUs from the
+// wrong node).
+bool numa_binding() {
+  static const bool on = [] {
+    const char *e = getenv("GLFSX_NUMA");
+    return !e || atoi(e) != 0;
   }();
-  return *p;
+  return on;
 }
 
-void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
+CopyPool &copy_pool(int dev = -1) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, CopyPool *>> pools;  // (node, pool), process lifetime
+  static std::vector<int> dev_node;                      // device -> node (-2: unknown yet)
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  int node = -1;
+  if (numa_binding()) {
+    if (size_t(dev) >= dev_node.size()) dev_node.resize(dev + 1, -2);
+    if (dev_node[dev] == -2) dev_node[dev] = device_numa_node(dev);
+    node = dev_node[dev];
+  }
+  for (auto &p : pools)
+    if (p.first == node) return *p.second;
+  auto *cp = new CopyPool();
+  const unsigned hw = std::thread::hardware_concurrency();
+  cp->workers = std::min(15u, hw > 1 ? hw - 1 : 0u);
+  cpu_set_t cpus;
+  const bool bind = node_cpus(node, &cpus);
+  for (unsigned i = 0; i < cp->workers; ++i)
+    std::thread([cp, bind, cpus] {
+      if (bind) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus, &cpus);
+      cp->run();
+    }).detach();
+  pools.push_back({node, cp});
+  return *cp;
+}
+
+// dev: the device whose staging dst is (-1: the current device), which
+// picks the copy pool of its NUMA node.
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n, int dev = -1) {
   constexpr size_t kPiece = 256u << 10;
   if (n < 2 * kPiece) {
     memcpy(dst, src, n);
     return;
   }
-  CopyPool &P = copy_pool();
+  CopyPool &P = copy_pool(dev);
   const size_t parts = std::min<size_t>(P.workers + 1, n / kPiece);
   if (parts <= 1) {
     memcpy(dst, src, n);
@@ -1035,9 +1052,9 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
 // memcpy.  Returns the bytes of the contiguous prefix read (< n only at the
 // end of the input) or the first piece's error (negative).
 int64_t par_read_at(glfsx_read_at_fn fn, void *ctx, uint8_t *dst, uint64_t n, uint64_t off,
-                    unsigned max_threads) {
+                    unsigned max_threads, int dev = -1) {
   constexpr uint64_t kPiece = 4ull << 20;
-  CopyPool &P = copy_pool();
+  CopyPool &P = copy_pool(dev);
   const uint64_t parts = std::max<uint64_t>(
       1, std::min<uint64_t>({uint64_t(P.workers) + 1, uint64_t(max_threads), n / kPiece}));
   if (parts <= 1) return read_full(fn, ctx, dst, n, off);
@@ -1077,7 +1094,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
              bool dev_src = false, const PinBuf *pin = nullptr,
              uint64_t present = ~0ull) {
   OneBuf &o = w->one;
-  if (!dev_src && n <= kMaxMedLen && one_enabled()) {
+  if (!dev_src && n <= kMaxMedLen) {
     if (int e = o.h_ct.ensure(n + 64)) return e;
     if (int e = o.h_ref.ensure(64)) return e;
     const uint64_t have = std::min(n, present);
@@ -1143,7 +1160,7 @@ int post_one(glfsx_writer *w, int kind, const uint8_t salt[32],
 int post_node(glfsx_writer *w, size_t i, uint8_t r[64]) {
   std::vector<uint8_t> &v = w->indexes[i];
   int e;
-  if (w->bs <= kMaxMedLen && one_enabled()) {  // the kernel reads the rest as zero
+  if (w->bs <= kMaxMedLen) {  // the kernel reads the rest as zero
     e = post_one(w, 1, w->salts.index, v.data(), w->bs, r, false, nullptr, v.size());
   } else {
     v.resize(w->bs, 0);
@@ -1373,6 +1390,13 @@ uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us) {
   return fused_timeouts();
 }
 
+int glfsx_clock_probe(int reset, uint64_t out[2]) {
+  Ctx *c;
+  if (int e = ctx_get(&c)) return e;
+  HIP_TRY(clock_probe(reset, out));
+  return 0;
+}
+
 #if GLFSX_WGTIME
 // diagnostic builds only (tools/build_variant.sh): the bulk passes' phase
 // timestamps, 8192 x 8 words
@@ -1488,7 +1512,7 @@ int glfsx_post(const uint8_t salt[32], const void *ptext, uint64_t n,
                 (unsigned long long)n, (unsigned long long)kMaxMsgLen);
   Ctx *c;
   if (int e = ctx_get(&c)) return e;
-  if (n <= kMaxMedLen && one_enabled()) {
+  if (n <= kMaxMedLen) {
     if (int e = c->h_oin.ensure(n + 64)) return e;
     if (int e = c->h_oct.ensure(n + 64)) return e;
     if (int e = c->h_oref.ensure(64)) return e;
@@ -1740,7 +1764,7 @@ constexpr uint64_t kFewBlocks = 8;
 int post_few(glfsx_writer *w, bool tail, bool *done) {
   *done = false;
   WSlot &sl = w->slot[w->cur];
-  if (!one_enabled() || sl.on_dev || w->full == 0 || w->full > kFewBlocks ||
+  if (sl.on_dev || w->full == 0 || w->full > kFewBlocks ||
       w->bs > kMaxMedLen || (w->bs & 15) || !sl.h_in.dp)
     return 0;
   if (int e = complete_all(w)) return e;
@@ -1808,7 +1832,7 @@ int glfsx_writer_write(glfsx_writer *w, const void *data, size_t n) {
     const uint64_t cap = w->batch_blocks * w->bs;  // slot holds up to a batch
     const uint64_t take = std::min<uint64_t>(cap - used, n);
     if (int e = pin_grow(sl.h_in, used + take, used)) return call.done(w->sticky = e);
-    par_memcpy(sl.h_in.u8() + used, p, take);
+    par_memcpy(sl.h_in.u8() + used, p, take, w->lanes[sl.lane].dev);
     p += take;
     n -= take;
     w->full = (used + take) / w->bs;
@@ -1893,7 +1917,7 @@ int glfsx_writer_read_at(glfsx_writer *w, glfsx_read_at_fn read_at, void *ctx,
     if (int e = pin_grow(sl.h_in, room, used)) return call.done(w->sticky = e);
     const uint64_t want = std::min(room - used, n - total);
     const int64_t r = par_read_at(read_at, ctx, sl.h_in.u8() + used, want, offset + total,
-                                  read_threads());
+                                  read_threads(), w->lanes[sl.lane].dev);
     if (r < 0) {
       rc = fail(GLFSX_E_IO, "read of %llu bytes at input offset %llu failed (%lld)",
                 (unsigned long long)want, (unsigned long long)(offset + total), (long long)r);
@@ -2773,7 +2797,7 @@ int glfsx_post_blobs(uint64_t block_size, uint64_t store_max, const uint8_t *sal
   for (uint64_t i = 0; i < n; ++i) {
     if (lengths[i] <= small_max) {
       ++n_small;
-    } else if (lengths[i] <= bs && lengths[i] <= kMaxMedLen && one_enabled()) {
+    } else if (lengths[i] <= bs && lengths[i] <= kMaxMedLen) {
       med.push_back(i);
     } else {
       glfsx_root r;
@@ -2875,16 +2899,21 @@ int glfsx_decrypt_batch_device(const void *d_ctext, uint64_t total,
 // PostTreeMap over n entries whose blobs are glfs.PostBlob'd (machine.go:64)
 // -- blob roots (glfsx_post_blobs_device), the tree's JSON lines
 // (glfsx_tree_encode_device) and the tree blob's Create
-// (glfsx_create_device) -- in one call: the lines' layout runs first (it
-// does not depend on the roots' values: hex fields are fixed width), then
-// the blobs hash and the lines are written, all queued before the host reads
-// the layout's total; the tree blob's blocks are posted on a second stream.
-// GLFSX_TREE_BATCHES > 1 hashes the entries in groups and posts each
-// group's finished tree blocks beside the next group (measured slower, see
-// `batches`).  Same bytes and roots as the three calls in sequence
-// (tests/test_gpu_tree_read.py).  Blobs above 16 KiB, a tree block size
-// that is not a multiple of 64, or no line buffer take the
-// three calls in sequence.
+// (glfsx_create_device) -- in one call, every launch queued before the host
+// waits:
+//   A: the blobs' DEK pass;
+//   B (beside it): the lines' layout (lengths, then a one-workgroup prefix
+//      that stores the total in a pinned word the host reads) and the lines
+//      without their hex digits, at raised wave priority (a hex field is
+//      fixed width, so the layout does not depend on the roots' values);
+//   A: the blobs' CID pass once the static lines are in, writing each
+//      root's hex digits into its line;
+//   A: the tree blob's blocks and index levels (glfsx_create_device's
+//      closed form) once the host has read the total.
+// Same bytes and roots as the three calls in sequence
+// (tests/test_gpu_tree_read.py).  Blobs above 16 KiB, a tree block size that
+// is not a multiple of 64, or no line buffer take the three calls in
+// sequence.
 namespace {
 int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt,
                           const uint8_t *tree_salt, const uint8_t *cid_key,
@@ -2899,16 +2928,6 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   if (!tree_root || !lines_len) return fail(GLFSX_E_ARG, "null argument");
   if (int e = check_block_size(blob_bs)) return e;
   if (int e = check_block_size(tree_bs)) return e;
-  static const uint64_t batches = [] {
-    const char *e = getenv("GLFSX_TREE_BATCHES");
-    // 1: one hashing launch pair for all entries.  Groups of entry
-    // workgroups let the tree blob's first blocks hash beside the next
-    // group, but each group's persistent passes end in their own tail and
-    // the tree posts compete with them for the chip: config 4 one call
-    // 750 / 716 / 677 GiB/s at 1 / 2 / 4 groups (3 interleaved reps,
-    // scripts/ab_small.py, profiles/r3/ab_tree_batches.log)
-    return std::max<uint64_t>(1, e ? strtoull(e, nullptr, 10) : 1);
-  }();
   if (n == 0 || max_len > small_max_for(blob_bs) || tree_bs % 64 || !d_lines) {
     if (int e = glfsx_post_blobs_device(blob_bs, blob_salt, cid_key, d_data, d_offsets,
                                         d_lengths, n, max_len, d_ctext, d_roots, stream))
@@ -2930,25 +2949,17 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
   hipStream_t B = c->stream2;
   const uint64_t wgs = (n + kTreeWG - 1) / kTreeWG;
-  const uint64_t K = std::min(batches, wgs);
-  // K == 1: the lines' static parts are written on B beside the blobs' DEK
-  // pass and the CID pass writes each root's hex digits into its line
-  // (GLFSX_TREE_HEX=0: the lines kernel after the hashing, A/B)
-  static const bool hex_fused = [] {
-    const char *e = getenv("GLFSX_TREE_HEX");
-    return !e || atoi(e) != 0;
-  }();
-  const bool fuse = hex_fused && K == 1;
-  while (c->events.size() < K + 4) {
+  while (c->events.size() < 3) {
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->events.push_back(ev);
   }
+  hipEvent_t ev_before = c->events[0], ev_layout = c->events[1], ev_static = c->events[2];
   Salts bsalts, tsalts;
   if (int e = derive_salts(c, blob_salt, &bsalts)) return e;
   if (int e = derive_salts(c, tree_salt, &tsalts)) return e;
   const uint64_t words = n + wgs + 1;
-  if (int e = c->d_tree.ensure(8 * (words + (fuse ? n : 0)))) return e;
+  if (int e = c->d_tree.ensure(8 * (words + n))) return e;
   if (int e = c->h_tree.ensure(8 * (wgs + 1))) return e;
   TreeJob tj{};
   tj.n = n;
@@ -2964,35 +2975,24 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   tj.total = tj.scratch + words - 1;
   tj.out = static_cast<uint8_t *>(d_lines);
   tj.cap = lines_cap;
-  // B's tree posts come after everything already on A
-  HIP_TRY(hipEventRecord(c->events[K], A));
-  HIP_TRY(hipStreamWaitEvent(B, c->events[K], 0));
-  static const bool half = [] {  // GLFSX_TREE_HALF=0: full workgroups (A/B)
-    const char *e = getenv("GLFSX_TREE_HALF");
-    return !e || atoi(e) != 0;
-  }();
-  // GLFSX_TREE_BESIDE (default 1; 0 = the first round-4 order, A/B): the
-  // layout runs on B beside the blobs' DEK pass as well, its prefix in one
-  // 256-thread workgroup and every layout / static-line wave at raised issue
-  // priority.  Otherwise the layout runs first on A (a 1024-thread prefix
-  // beside the DEK pass waits for a CU until the pass drains) and the static
-  // lines, at the oldest-first SIMD's leftover issue, ended 74 us after the
-  // DEK pass (0.09 ms before the CID pass could start; profiles/r4/
-  // c4_timeline.txt).
-  static const bool beside_env = [] {
-    const char *e = getenv("GLFSX_TREE_BESIDE");
-    return !e || atoi(e) != 0;
-  }();
-  static const bool prio_env = [] {  // GLFSX_TREE_PRIO=0: no raised priority (A/B)
-    const char *e = getenv("GLFSX_TREE_PRIO");
-    return !e || atoi(e) != 0;
-  }();
-  const bool beside = fuse && half && beside_env;
+  tj.hex_pos = tj.scratch + words;  // where each root's digits go
+  tj.prio = 1;                      // beside the DEK pass: raised issue priority
+  // the prefix stores the exclusive prefixes and the total in the pinned
+  // words the host reads (a copy kernel behind it on B would wait for a CU
+  // beside the DEK pass -- 1.1 ms in the round-4 trace)
+  tj.prefix_host = reinterpret_cast<uint64_t *>(c->h_tree.dptr());
+  // B's work comes after everything already on A
+  HIP_TRY(hipEventRecord(ev_before, A));
+  HIP_TRY(hipStreamWaitEvent(B, ev_before, 0));
   SmallJob sj{};
   sj.src = static_cast<const uint8_t *>(d_data);
   sj.ctext = static_cast<uint8_t *>(d_ctext);
   sj.max_len = max_len;
   sj.small_max = small_max_for(blob_bs);
+  sj.offs = d_offsets;
+  sj.lens = d_lengths;
+  sj.n = n;
+  sj.refs = static_cast<uint8_t *>(d_roots);
   words_from_key(sj.raw_salt, bsalts.raw);
   words_from_key(sj.index_salt, bsalts.index);
   if (cid_key) {
@@ -3001,193 +3001,54 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   } else {
     blake3_iv_words(sj.cid_key);
   }
-  static const bool dek_first_env = [] {  // GLFSX_DEK_FIRST=0: the layout first (A/B)
-    const char *e = getenv("GLFSX_DEK_FIRST");
-    return !e || atoi(e) != 0;
-  }();
-  const bool dek_first = beside && dek_first_env;
-  if (dek_first) {
-    // the blobs' DEK pass (the critical path) queued first; the layout and
-    // static lines follow on B beside it, then the CID pass below
-    sj.offs = d_offsets;
-    sj.lens = d_lengths;
-    sj.n = n;
-    sj.refs = static_cast<uint8_t *>(d_roots);
-    sj.passes = 1;
-    HIP_TRY(launch_post_small(sj, A));
-  }
-  hipStream_t L = beside ? B : A;  // the layout's stream
-  tj.prio = beside ? (prio_env ? 1u : 2u) : 0u;
-  if (beside) {
-    // one group needs only the total: the prefix kernel stores it in the
-    // pinned word the host reads (a copy kernel behind it on B would wait
-    // for a CU beside the DEK pass -- 1.1 ms in the trace -- and the static
-    // lines behind the copy)
-    tj.prefix_host = reinterpret_cast<uint64_t *>(c->h_tree.dptr());
-    HIP_TRY(launch_tree_layout(tj, L));
-  } else {
-    HIP_TRY(launch_tree_layout(tj, L));
-    // exclusive prefix per entry workgroup, then the total (one copy)
-    HIP_TRY(hipMemcpyAsync(c->h_tree.p, tj.scratch + n, 8 * (wgs + 1), hipMemcpyDeviceToHost,
-                           L));
-  }
-  HIP_TRY(hipEventRecord(c->events[K + 1], L));
-  hipEvent_t static_done = nullptr;
-  if (fuse) {
-    // B: the lines without their hex digits, and where each root's digits go
-    tj.hex_pos = tj.scratch + words;
-    if (!beside) HIP_TRY(hipStreamWaitEvent(B, c->events[K + 1], 0));
-    if (half)
-      HIP_TRY(launch_tree_static(tj, B));
-    else
-      HIP_TRY(launch_tree_write(tj, 0, wgs, B));
-    static_done = c->events[K + 2];
-    HIP_TRY(hipEventRecord(static_done, B));
-  }
-  // GLFSX_TREE_SPLIT=P (1-99; default 0 = off, measured slower): with the
-  // layout beside, the CID pass runs as two launches, the first P % of the
-  // entry workgroups, then the rest on 3/4 of the chip; the tree blocks
-  // whose lines are complete after the first (their bytes end before the
-  // first entry of the second) are posted on B beside the second, and only
-  // the last few blocks -- a split plan of short lanes -- and the index node
-  // remain after it.  In the trace the tree blocks' DEK pass on B got almost
-  // no CU time beside the second group (571 us instead of 105) and the
-  // second group ran slower on 3/4 of the chip: config 4 820 / 823 GiB/s at
-  // P = 85 / 70 vs 836 unsplit.
-  static const uint64_t split_env = [] {
-    const char *e = getenv("GLFSX_TREE_SPLIT");
-    return e ? strtoull(e, nullptr, 10) : 0ull;
-  }();
-  const uint64_t g_split = (beside && dek_first && split_env > 0 && split_env < 100 && wgs >= 8)
-                               ? std::max<uint64_t>(1, wgs * split_env / 100) : 0;
-  if (g_split) {
-    const uint64_t e1 = g_split * kTreeWG;
-    sj.hex_out = static_cast<uint8_t *>(d_lines);
-    sj.hex_pos = tj.hex_pos;
-    sj.passes = 2;
-    sj.offs = d_offsets;
-    sj.lens = d_lengths;
-    sj.n = e1;
-    sj.refs = static_cast<uint8_t *>(d_roots);
-    sj.cid_wait = static_done;
-    HIP_TRY(launch_post_small(sj, A));
-    HIP_TRY(hipEventRecord(c->events[K + 3], A));  // the first group's lines are done
-    sj.offs = d_offsets + e1;
-    sj.lens = d_lengths + e1;
-    sj.n = n - e1;
-    sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e1;
-    sj.hex_pos = tj.hex_pos + e1;  // indexed by the group's own blob numbers
-    sj.cid_wait = nullptr;
-    sj.quarters = 3;
-    HIP_TRY(launch_post_small(sj, A));
-    HIP_TRY(hipEventRecord(c->events[0], A));
-  }
-  // every group's hashing and lines queued on A before the host waits for
-  // the layout (k_tree_write skips its work when the lines exceed the cap)
-  for (uint64_t b = 0; b < K && !g_split; ++b) {
-    const uint64_t g0 = wgs * b / K, g1 = wgs * (b + 1) / K;
-    const uint64_t e0 = g0 * kTreeWG, e1 = std::min(n, g1 * kTreeWG);
-    sj.offs = d_offsets + e0;
-    sj.lens = d_lengths + e0;
-    sj.n = e1 - e0;
-    sj.refs = static_cast<uint8_t *>(d_roots) + 64 * e0;
-    if (fuse) {  // the CID pass writes the digits once the static parts are in
-      sj.hex_out = static_cast<uint8_t *>(d_lines);
-      sj.hex_pos = tj.hex_pos;
-      sj.cid_wait = static_done;
-      sj.passes = dek_first ? 2u : 0u;  // (the DEK pass may be queued already)
-      HIP_TRY(launch_post_small(sj, A));
-    } else {
-      HIP_TRY(launch_post_small(sj, A));
-      HIP_TRY(launch_tree_write(tj, g0, g1, A));
-    }
-    HIP_TRY(hipEventRecord(c->events[b], A));
-  }
-  HIP_TRY(hipEventSynchronize(c->events[K + 1]));
-  const uint64_t *prefix = static_cast<const uint64_t *>(c->h_tree.p);
-  const uint64_t total = prefix[wgs];
+  sj.passes = 1;  // the DEK pass: the critical path, queued first
+  HIP_TRY(launch_post_small(sj, A));
+  HIP_TRY(launch_tree_layout(tj, B));
+  HIP_TRY(hipEventRecord(ev_layout, B));
+  HIP_TRY(launch_tree_static(tj, B));
+  HIP_TRY(hipEventRecord(ev_static, B));
+  sj.passes = 2;  // the CID pass, writing the digits once the static parts are in
+  sj.hex_out = static_cast<uint8_t *>(d_lines);
+  sj.hex_pos = tj.hex_pos;
+  sj.cid_wait = ev_static;
+  HIP_TRY(launch_post_small(sj, A));
+  HIP_TRY(hipEventSynchronize(ev_layout));
+  const uint64_t total = static_cast<const uint64_t *>(c->h_tree.p)[wgs];
   if (total > lines_cap) {
     HIP_TRY(hipStreamSynchronize(A));
     *lines_len = total;
     return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
                 (unsigned long long)total, (unsigned long long)lines_cap);
   }
+  // the tree blob, on A after the CID pass (its lines are complete then)
   const uint64_t nblk = (total + tree_bs - 1) / tree_bs;
-  // the tree blob's posts: with one group (the lines complete when A's CID
-  // pass ends) on A itself, after it -- no cross-stream event in the chain;
-  // with several groups on B, each group's blocks beside the next group
-  static const bool on_a_env = [] {  // GLFSX_TREE_ON_A=0: on B (A/B)
-    const char *e = getenv("GLFSX_TREE_ON_A");
-    return !e || atoi(e) != 0;
-  }();
-  const hipStream_t T = (fuse && on_a_env) ? A : B;
-  // split CID pass: the blocks complete after its first group go on B
-  const uint64_t t_split = g_split ? std::min(prefix[g_split] / tree_bs, nblk) : 0;
-  hipStream_t P = t_split ? B : T;  // the level buffer's preparation
-  if (t_split) HIP_TRY(hipStreamWaitEvent(B, c->events[K + 3], 0));
-  if (int e = level_prepare(c->d_lvl_a, nblk, (nblk + tree_bs / 64 - 1) / (tree_bs / 64),
-                            tree_bs, P))
-    return e;
+  const uint64_t n1 = (nblk + tree_bs / 64 - 1) / (tree_bs / 64);
+  if (int e = level_prepare(c->d_lvl_a, nblk, n1, tree_bs, A)) return e;
   uint8_t *lvl = c->d_lvl_a.u8();
-  auto post_tree_blocks = [&](uint64_t t0, uint64_t t1, hipStream_t s) -> int {
-    PostJob j{};
-    j.src = static_cast<const uint8_t *>(d_lines) + t0 * tree_bs;
-    j.ctext = d_tree_ctext ? static_cast<uint8_t *>(d_tree_ctext) + t0 * tree_bs : nullptr;
-    j.stride = tree_bs;
-    j.msg_len = tree_bs;
-    j.n = t1 - t0;
-    j.last_len = t1 == nblk ? total - (nblk - 1) * tree_bs : tree_bs;
-    j.out = RefLayout{lvl + 64 * t0, ~0ull, 0};  // ref t at byte 64t
-    words_from_key(j.salt, tsalts.raw);
-    cid_words(j, cid_key);
-    HIP_TRY(launch_post(j, s, tls_fused));
-    return 0;
-  };
-  if (g_split) {
-    if (t_split) {
-      if (int e = post_tree_blocks(0, t_split, B)) return e;
-      HIP_TRY(hipEventRecord(c->events[K + 3], B));
-    }
-    if (t_split < nblk)  // on A after the second group (few blocks: short lanes)
-      if (int e = post_tree_blocks(t_split, nblk, A)) return e;
-    if (t_split) HIP_TRY(hipStreamWaitEvent(A, c->events[K + 3], 0));
-  }
-  // on T: each tree block once all its bytes are written
-  uint64_t t_done = 0;
-  for (uint64_t b = 0; b < K && !g_split; ++b) {
-    const uint64_t g1 = wgs * (b + 1) / K;
-    const uint64_t ready = b + 1 == K ? total : prefix[g1];
-    const uint64_t t_ready = b + 1 == K ? nblk : ready / tree_bs;
-    if (T != A) HIP_TRY(hipStreamWaitEvent(T, c->events[b], 0));
-    if (t_ready > t_done) {
-      if (int e = post_tree_blocks(t_done, t_ready, T)) return e;
-      t_done = t_ready;
-    }
-  }
+  PostJob j{};
+  j.src = static_cast<const uint8_t *>(d_lines);
+  j.ctext = static_cast<uint8_t *>(d_tree_ctext);
+  j.stride = tree_bs;
+  j.msg_len = tree_bs;
+  j.n = nblk;
+  j.last_len = total - (nblk - 1) * tree_bs;
+  j.out = RefLayout{lvl, ~0ull, 0};  // ref t at byte 64t
+  words_from_key(j.salt, tsalts.raw);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, A, tls_fused));
   *lines_len = total;
   tree_root->size = total;
   tree_root->block_size = tree_bs;
   if (nblk <= 1) {  // one block: its ref is the root (blob.go:190-193)
     if (int e = c->h_root.ensure(64)) return e;
-    HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, T));
-    HIP_TRY(stream_wait(T));
-    if (T != B) HIP_TRY(stream_wait(B));
-    if (int e = fused_check(T)) return e;
-    if (T != B)
-      if (int e = fused_check(B)) return e;
+    HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, A));
+    HIP_TRY(stream_wait(A));  // (B is drained: A waited for its static lines)
+    if (int e = fused_check(A)) return e;
     memcpy(tree_root->ref, c->h_root.p, 64);
     return 0;
   }
   uint64_t posts = 0;
-  if (int e = build_up(c, T, tsalts, cid_key, tree_bs, lvl,
-                       (nblk + tree_bs / 64 - 1) / (tree_bs / 64), &c->d_lvl_b,
-                       tree_root->ref, &posts))
-    return e;
-  if (T != B) {
-    HIP_TRY(stream_wait(B));  // (drained already: A waited for B's work)
-    if (int e = fused_check(B)) return e;  // tree posts on B (split CID pass)
-  }
-  return 0;
+  return build_up(c, A, tsalts, cid_key, tree_bs, lvl, n1, &c->d_lvl_b, tree_root->ref, &posts);
 }
 }  // namespace
 

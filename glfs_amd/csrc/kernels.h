@@ -49,6 +49,11 @@ uint32_t fused_errors_take(hipStream_t s);
 void fused_debug(uint32_t skip_msg, uint64_t wait_us);
 // Timeouts seen by fused_errors_take so far (process-wide).
 uint64_t fused_timeouts();
+// The bulk passes' clock probe on the current device (k_pass): out[0] =
+// shader-clock cycles, out[1] = 100 MHz ticks summed over every k_pass
+// workgroup since the last reset; reset: zero them after reading.
+// Synchronous (waits for the device).
+hipError_t clock_probe(int reset, uint64_t out[2]);
 
 // The second half of launch_post alone: ChaCha20 keyed by the DEK already in
 // bytes [32,64) of each ref slot, ctext store, CID into bytes [0,32).
@@ -89,8 +94,6 @@ struct SmallJob {
   const uint64_t *hex_pos;
   hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
   uint32_t passes;      // 1: the DEK pass only, 2: the CID pass only, 0: both
-  uint32_t quarters;    // k_small_q's grid: this many quarters of what the
-                        // chip holds (0: all), leaving room for other work
 };
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
@@ -169,8 +172,8 @@ struct TreeJob {
   // first cid digit (its dek digits start kDekAfterCid bytes later); the
   // small-blob CID pass writes them (SmallJob::hex_out)
   uint64_t *hex_pos;
-  // nonzero: the layout and static-line kernels run beside the small-blob
-  // DEK pass (a 256-thread prefix; 1: also at raised wave priority)
+  // 1: the layout and static-line kernels run beside the small-blob DEK
+  // pass (a 256-thread prefix, raised wave priority)
   uint32_t prio;
   // nullable, pinned host memory (device pointer) of ceil(n / 256) + 1
   // words: the layout's prefix kernel also stores the per-workgroup
@@ -183,9 +186,8 @@ constexpr uint32_t kDekAfterCid = 64 + 9;
 hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s);
 // The same in two steps: the layout (line lengths, per-workgroup exclusive
 // prefix at scratch + n, the total) -- it does not read the roots' values --
-// and the lines of entry workgroups [wg0, wg1) (kTreeWG entries each).
+// and then the static lines (launch_tree_static).
 hipError_t launch_tree_layout(const TreeJob &j, hipStream_t s);
-hipError_t launch_tree_write(const TreeJob &j, uint64_t wg0, uint64_t wg1, hipStream_t s);
 // The lines without their hex digits (j.hex_pos set), in half workgroups
 // small enough to run beside the small-blob DEK pass.
 hipError_t launch_tree_static(const TreeJob &j, hipStream_t s);

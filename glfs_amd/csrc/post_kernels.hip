@@ -1215,10 +1215,26 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   WGT(bid, 3);
 }
 
+// Clock probe of the bulk passes (glfsx_clock_probe): every k_pass
+// workgroup adds its lifetime in shader-clock cycles (s_memtime) and in
+// 100 MHz ticks (s_memrealtime) to these two device words, so a caller reads
+// the clock the chip held over exactly the launches it timed:
+// cycles / ticks x 100 MHz.  Two scalar timer reads per wave and two atomic
+// adds per workgroup (thread 0).
+__device__ unsigned long long g_clk[2];
+
 template <int G, bool CHACHA, bool ALIGNED, int A = 2>
 __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   __shared__ uint4 lds_u4[512 + kStageOf<CHACHA>];
+  const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr);
+  if (threadIdx.x == 0) {
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_add(&g_clk[0], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&g_clk[1], (unsigned long long)(r1 - r0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Both passes of a split-mode post in one launch: the DEK items run the DEK
@@ -2365,19 +2381,11 @@ hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
 }
 
 // Split-mode target: workgroups per launch below which a message is spread
-// over more workgroups (fewer chunks per lane).  0 disables split mode.
-// GLFSX_SPLIT_WG overrides the default (tuning, A/B runs).
-uint32_t split_target_default() {
-  const char *e = getenv("GLFSX_SPLIT_WG");
-  return e ? uint32_t(strtoul(e, nullptr, 10)) : 2048u;
-}
-std::atomic<uint32_t> g_split_target{split_target_default()};
+// over more workgroups (fewer chunks per lane).  0 disables split mode
+// (glfsx_set_split_target: tests of both forms).
+std::atomic<uint32_t> g_split_target{2048u};
 constexpr uint32_t kMaxSplitLog2 = 8;  // the last workgroup merges <= 256 CVs
-// see pass_plan; GLFSX_DC_MIN overrides (0: the round-3 plans, A/B)
-const uint64_t kDcMinWgs = [] {
-  const char *e = getenv("GLFSX_DC_MIN");
-  return e ? uint64_t(strtoull(e, nullptr, 10)) : uint64_t(1024);
-}();
+constexpr uint64_t kDcMinWgs = 1024;   // see pass_plan
 
 // Split-mode scratch (32 B per workgroup) and arrival counters (4 B per
 // message, zero between launches: each message's last workgroup resets its
@@ -2614,27 +2622,12 @@ void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   *sl_out = sl;
 }
 
-bool quad_enabled() {
-  static const bool on = [] {
-    const char *e = getenv("GLFSX_QUAD");
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
-
 // BLAKE3-only pass in quad layout (k_quad): latency-bound launches of at
 // most 16384 chunks, messages of at most 64 x 256 KiB.  Messages of up to
 // 64 x 64 KiB (4 MiB: index nodes at 1-4 MiB blocks) use 64 quads per
 // workgroup, larger ones 256 (the last workgroup merges <= 64 CVs, one per
-// quad of its own).  GLFSX_QPW=256 forces the wide form (A/B).
-int quad_qpw(uint64_t maxlen) {
-  static const int forced = [] {
-    const char *e = getenv("GLFSX_QPW");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 256) return 256;
-  return maxlen <= (64ull << 16) ? 64 : 256;
-}
+// quad of its own).
+int quad_qpw(uint64_t maxlen) { return maxlen <= (64ull << 16) ? 64 : 256; }
 
 hipError_t launch_quad(KArgs a, uint64_t maxlen, hipStream_t s) {
   const int qpw = quad_qpw(maxlen);
@@ -2660,7 +2653,7 @@ bool quad_ok(const KArgs &a, uint64_t maxlen, bool aligned, uint32_t sl) {
   const uint64_t chunks = a.n * (maxlen ? (maxlen + 1023) >> 10 : 1);
   const bool refs4 = ((reinterpret_cast<uintptr_t>(a.refs) | a.out_off |
                        a.ref_stride) & 3) == 0;
-  return quad_enabled() && aligned && refs4 && (a.n << sl) <= latency_wgs() &&
+  return aligned && refs4 && (a.n << sl) <= latency_wgs() &&
          chunks <= 16384 && maxlen <= (64ull * 256) << 10;
 }
 
@@ -2731,14 +2724,6 @@ hipError_t small_q_get(hipStream_t s, uint32_t **ctr, uint32_t *epoch) {
   return hipSuccess;
 }
 
-bool small_q_enabled() {
-  static const bool on = [] {
-    const char *e = getenv("GLFSX_SMALL_Q");
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
-
 // Workgroups of kernel k the whole chip holds at once.
 template <class K>
 uint32_t resident_wgs(K k) {
@@ -2750,27 +2735,20 @@ uint32_t resident_wgs(K k) {
   return uint32_t(std::max(per_cu, 1) * std::max(cus, 1));
 }
 
-// GLFSX_SMALL_FINE: k_small_q hands out the last 1/div of the blobs as fine
-// items (0: none).  1 M x 4 KiB blobs, 3 interleaved reps: small blobs 911 /
-// 919 / 926 GiB/s at 0 / 4 / 8, config 4 end to end 780 / 791 / 801.
-uint32_t small_fine_div() {
-  static const uint32_t v = [] {
-    const char *e = getenv("GLFSX_SMALL_FINE");
-    return e ? uint32_t(strtoul(e, nullptr, 10)) : 8u;
-  }();
-  return v;
-}
+// k_small_q hands out the last 1/kSmallFineDiv of the blobs as fine items.
+// 1 M x 4 KiB blobs, 3 interleaved reps: small blobs 911 / 919 / 926 GiB/s
+// at none / 1/4 / 1/8, config 4 end to end 780 / 791 / 801.
+constexpr uint32_t kSmallFineDiv = 8;
 
 template <int G, bool CHACHA, int A>
-hipError_t launch_small_q(const SArgs &a0, hipStream_t s, uint32_t quarters) {
-  static const uint32_t all = resident_wgs(k_small_q<G, CHACHA, A>);
-  const uint32_t slots = (quarters && all) ? std::max(1u, all / 4 * quarters) : all;
+hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
+  static const uint32_t slots = resident_wgs(k_small_q<G, CHACHA, A>);
   uint32_t *ctr;
   uint32_t epoch;
   hipError_t e = small_q_get(s, &ctr, &epoch);
   if (e != hipSuccess) return e;
   SArgs a = a0;
-  const uint32_t div = G > 1 ? small_fine_div() : 0u;
+  const uint32_t div = G > 1 ? kSmallFineDiv : 0u;
   const uint64_t fine = div ? a.n / div : 0;
   a.n_coarse = (a.n - fine) >> 6;  // whole coarse items; the rest goes fine
   const uint64_t rest = a.n - (a.n_coarse << 6), bpi = G > 1 ? 64 / G : 64;
@@ -2782,8 +2760,7 @@ hipError_t launch_small_q(const SArgs &a0, hipStream_t s, uint32_t quarters) {
 }
 
 template <bool CHACHA>
-hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s,
-                             uint32_t quarters = 0) {
+hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
   const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
   const int gsel = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0;
@@ -2798,27 +2775,17 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s,
     }
     return hipGetLastError();
   }
-  // ARX form of the many-wave small-blob kernels (GLFSX_SMALL_DEK / _CID)
+  // more workgroups than the chip holds: per-wave items (k_small_q), in the
+  // ARX form GLFSX_SMALL_DEK / _CID
   constexpr int F = CHACHA ? GLFSX_SMALL_CID : GLFSX_SMALL_DEK;
-  if (small_q_enabled()) {  // more workgroups than the chip holds: per-wave items
-    switch (gsel) {
-      case 1: return launch_small_q<1, CHACHA, F>(a, s, quarters);
-      case 2: return launch_small_q<2, CHACHA, F>(a, s, quarters);
-      case 4: return launch_small_q<4, CHACHA, F>(a, s, quarters);
-      case 8: return launch_small_q<8, CHACHA, F>(a, s, quarters);
-      case 16: return launch_small_q<16, CHACHA, F>(a, s, quarters);
-      default: return hipErrorInvalidValue;
-    }
-  }
   switch (gsel) {
-    case 1: hipLaunchKernelGGL((k_small<1, CHACHA, F>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_small<2, CHACHA, F>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_small<4, CHACHA, F>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_small<8, CHACHA, F>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_small<16, CHACHA, F>), grid, block, 0, s, a); break;
+    case 1: return launch_small_q<1, CHACHA, F>(a, s);
+    case 2: return launch_small_q<2, CHACHA, F>(a, s);
+    case 4: return launch_small_q<4, CHACHA, F>(a, s);
+    case 8: return launch_small_q<8, CHACHA, F>(a, s);
+    case 16: return launch_small_q<16, CHACHA, F>(a, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 KArgs make_args(const PostJob &job) {
@@ -2918,31 +2885,16 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
   return launch_pass<false>(a, maxlen, is_aligned(job), s);
 }
 
-// GLFSX_DC_FINE: the fine-item share of k_pass_dc's CID items (the last
-// ceil(m / div) messages of each work list; 0: none)
-uint32_t dc_fine_div() {
-  static const uint32_t v = [] {
-    const char *e = getenv("GLFSX_DC_FINE");
-    return e ? uint32_t(strtoul(e, nullptr, 10)) : 4u;
-  }();
-  return v;
-}
-
-// GLFSX_FUSED=0: split-mode posts as two launches (DEK pass, then CID pass)
-bool fused_enabled() {
-  static const bool on = [] {
-    const char *e = getenv("GLFSX_FUSED");
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
+// The fine-item share of k_pass_dc's CID items: the last ceil(m / 4)
+// messages of each work list.
+constexpr uint32_t kDcFineDiv = 4;
 
 // Split-mode post of many-wave size in one launch (k_pass_dc): both passes
 // of launch_keyed_hash + launch_cid_pass when each would be one k_pass<G,
 // CHACHA, true, 2> launch with the same plan.
 hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   *done = false;
-  if (!fused_enabled() || job.n < 2 || !is_aligned(job)) return hipSuccess;
+  if (job.n < 2 || !is_aligned(job)) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(job.out.refs) | job.out.stride) & 3) return hipSuccess;
   const uint64_t maxlen = std::max(job.msg_len, job.last_len);
   int g;
@@ -2970,7 +2922,7 @@ hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   if (e != hipSuccess) return e;
   d.n = uint32_t(job.n);
   d.sl = sl;
-  d.fine_div = (g > 1 && sl < kMaxSplitLog2) ? dc_fine_div() : 0u;
+  d.fine_div = (g > 1 && sl < kMaxSplitLog2) ? kDcFineDiv : 0u;
   KArgs b = a;
   for (int i = 0; i < 8; ++i) b.key[i] = job.cid_key[i];
   b.base = job.cid_keyed ? kKeyed : 0u;
@@ -3089,7 +3041,20 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
     e = hipStreamWaitEvent(s, job.cid_wait, 0);
     if (e != hipSuccess) return e;
   }
-  return launch_small_pass<true>(a, max_len, s, job.quarters);
+  return launch_small_pass<true>(a, max_len, s);
+}
+
+hipError_t clock_probe(int reset, uint64_t out[2]) {
+  unsigned long long v[2] = {0, 0};
+  hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_clk), sizeof v, 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  if (out) {
+    out[0] = v[0];
+    out[1] = v[1];
+  }
+  if (!reset) return hipSuccess;
+  const unsigned long long z[2] = {0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof z, 0, hipMemcpyHostToDevice);
 }
 
 #if GLFSX_WGTIME

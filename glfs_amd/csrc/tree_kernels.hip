@@ -44,7 +44,7 @@ struct TArgs {
   uint64_t cap;         // bytes at out; nothing is written if the total exceeds it
   const uint64_t *total;
   uint64_t *hex_pos;    // nullable: skip the hex digits, record where they go
-  uint32_t prio;        // nonzero: the waves raise their issue priority
+  uint32_t prio;        // 1: the waves raise their issue priority
 };
 
 constexpr uint32_t kImg = 60 * 1024;  // LDS image per workgroup
@@ -342,12 +342,10 @@ __global__ __launch_bounds__(T) void k_tree_prefix(uint64_t *t, uint64_t m, uint
   }
 }
 
-// wg0: the first entry workgroup of this launch (a range of them is written
-// as soon as its entries' roots exist: glfsx_post_tree_device).
-__global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a, uint32_t wg0) {
+__global__ __launch_bounds__(kTreeWG) void k_tree_write(TArgs a) {
   __shared__ uint4 img4[kImg / 16];
   uint8_t *img = reinterpret_cast<uint8_t *>(img4);
-  const uint64_t wg = uint64_t(blockIdx.x) + wg0;
+  const uint64_t wg = blockIdx.x;
   const uint64_t i = wg * kTreeWG + threadIdx.x;
   const uint64_t last = min<uint64_t>(wg * kTreeWG + kTreeWG - 1, a.n - 1);
   const uint64_t base = a.wg_total[wg];           // exclusive prefix
@@ -519,13 +517,6 @@ hipError_t launch_tree_static(const TreeJob &j, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_tree_write(const TreeJob &j, uint64_t wg0, uint64_t wg1, hipStream_t s) {
-  if (j.n == 0 || wg1 <= wg0 || !j.out) return hipSuccess;
-  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wg1 - wg0)), dim3(kTreeWG), 0, s,
-                     tree_args(j), uint32_t(wg0));
-  return hipGetLastError();
-}
-
 hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
   if (j.n == 0) return hipSuccess;
   const TArgs a = tree_args(j);
@@ -537,7 +528,7 @@ hipError_t launch_tree_encode(const TreeJob &j, hipStream_t s) {
                      j.total, 0u, static_cast<uint64_t *>(nullptr));
   e = hipGetLastError();
   if (e != hipSuccess || !j.out) return e;
-  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a, 0u);
+  hipLaunchKernelGGL(k_tree_write, dim3(uint32_t(wgs)), dim3(kTreeWG), 0, s, a);
   return hipGetLastError();
 }
 

@@ -117,6 +117,15 @@ uint32_t glfsx_set_latency_wgs(uint32_t wgs);
  * number of failed one-launch posts seen so far, process-wide. */
 uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);
 
+/* Measurement hook (no reference counterpart): the bulk hashing passes
+ * (one workgroup per block) add each workgroup's lifetime in shader-clock
+ * cycles (out[0]) and in 100 MHz real-time ticks (out[1]) to two counters
+ * on the device; out[0] / out[1] x 0.1 GHz is the clock the chip held over
+ * the launches since the last reset (bench.py's VALU roofline).  Reads the
+ * calling thread's device, waiting for it; reset != 0 zeroes the counters
+ * after reading.  out may be NULL. */
+int glfsx_clock_probe(int reset, uint64_t out[2]);
+
 /* --- primitives -------------------------------------------------------- */
 /* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input (any length),
  * the first out_len bytes of the XOF (any length; blake3.New(len(out), salt)

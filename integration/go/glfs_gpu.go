@@ -182,13 +182,7 @@ func (ag *Machine) PostTreeMapGPU(ctx context.Context, s schema.WO, m map[string
 		ents = append(ents, TreeEntry{Name: p, FileMode: getFileMode(v), Ref: v})
 	}
 	SortTreeEntries(ents)
-	for i := 1; i < len(ents); i++ {
-		if ents[i].Name <= ents[i-1].Name { // tree.go:301-303
-			return nil, fmt.Errorf("cannot write tree entries out of order %q <= %q",
-				ents[i].Name, ents[i-1].Name)
-		}
-	}
-	if err := existsAll(ctx, s, ents); err != nil {
+	if err := checkEntries(ctx, s, ents); err != nil {
 		return nil, err
 	}
 	lines, ends, err := encodeTreeLines(ents)
@@ -214,10 +208,20 @@ func (ag *Machine) PostTreeMapGPU(ctx context.Context, s schema.WO, m map[string
 	return ag.PostTyped(ctx, s, TypeTree, bytes.NewReader(lines))
 }
 
-// existsAll is TreeWriter.Put's ExistsUnit check (tree.go:304-308) for every
-// entry, in batches of the store's Exists.
-func existsAll(ctx context.Context, s schema.WO, ents []TreeEntry) error {
+// checkEntries is TreeWriter.Put's two checks (tree.go:300-308) for every
+// entry in sorted order, one entry at a time as Put makes them: the name
+// order against the previous entry, then ExistsUnit.  Existence is asked in
+// batches of the store's Exists, but the first failure by entry index is
+// reported, whichever check it is, so the error is Put's (ADVICE r4).
+func checkEntries(ctx context.Context, s schema.WO, ents []TreeEntry) error {
 	const batch = 4096
+	order := func(i int) error {
+		if i > 0 && ents[i].Name <= ents[i-1].Name { // tree.go:301-303
+			return fmt.Errorf("cannot write tree entries out of order %q <= %q",
+				ents[i].Name, ents[i-1].Name)
+		}
+		return nil
+	}
 	cids := make([]blobcache.CID, 0, batch)
 	yes := make([]bool, batch)
 	for i0 := 0; i0 < len(ents); i0 += batch {
@@ -227,10 +231,16 @@ func existsAll(ctx context.Context, s schema.WO, ents []TreeEntry) error {
 			cids = append(cids, e.Ref.CID)
 		}
 		if err := s.Exists(ctx, cids, yes[:len(cids)]); err != nil {
-			return err
+			if oerr := order(i0); oerr != nil { // Put checks the order first
+				return oerr
+			}
+			return err // Put's first ExistsUnit fails the same way
 		}
 		for k, ok := range yes[:len(cids)] {
-			if !ok {
+			if err := order(i0 + k); err != nil {
+				return err
+			}
+			if !ok { // tree.go:304-308
 				return fmt.Errorf("adding tree ent %v would violate referential integrity",
 					ents[i0+k])
 			}

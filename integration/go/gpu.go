@@ -89,6 +89,7 @@ import (
 	"strconv"
 	"strings"
 	"sync"
+	"sync/atomic"
 	"unsafe"
 
 	"blobcache.io/blobcache/src/bcsdk"
@@ -211,11 +212,29 @@ func (gw *gpuWriter) Write(data []byte) (int, error) {
 	return len(data), nil
 }
 
+// osFile is what ReadFrom needs of a file: matched as an interface, not as
+// *os.File, because since Go 1.22 io.Copy(w, f) calls f.WriteTo, which for a
+// writer that is not a socket calls io.Copy(w, fileWithoutWriteTo{f}) -- a
+// wrapper embedding *os.File, so ReadFrom never sees the *os.File itself but
+// the wrapper has these methods (ADVICE r4).
+type osFile interface {
+	Fd() uintptr
+	Stat() (os.FileInfo, error)
+	io.Seeker
+}
+
+// fdRouteReads counts ReadFrom calls served by the pread route (gpu_test.go).
+var fdRouteReads uint64
+
+// gpuDeviceCount is glfsx_device_count for the tests (no cgo in _test.go).
+func gpuDeviceCount() int { return int(C.glfsx_device_count()) }
+
 // ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341).
-//   - A regular *os.File: read from its current offset to its end by the
-//     library's reader threads with pread(2), straight into the writer's
-//     pinned staging, while earlier batches hash (glfsx_writer_read_fd); the
-//     file is left positioned after what was read, as io.Copy leaves it.
+//   - A regular file (an *os.File, or io.Copy's fileWithoutWriteTo wrapper
+//     of one): read from its current offset to its end by the library's
+//     reader threads with pread(2), straight into the writer's pinned
+//     staging, while earlier batches hash (glfsx_writer_read_fd); the file
+//     is left positioned after what was read, as io.Copy leaves it.
 //   - An io.ReaderAt that is also an io.Seeker (*io.SectionReader, ...): the
 //     same through ReadAt from several threads (glfsx_writer_read_at).
 //   - Any other reader fills the staging directly, one Read at a time
@@ -224,10 +243,11 @@ func (gw *gpuWriter) Write(data []byte) (int, error) {
 //     Write.  C memory handed to Go as a slice is fine under the cgo rules;
 //     it is not used after commit.
 func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
-	if f, ok := r.(*os.File); ok {
+	if f, ok := r.(osFile); ok {
 		if st, err := f.Stat(); err == nil && st.Mode().IsRegular() {
 			if pos, err := f.Seek(0, io.SeekCurrent); err == nil {
 				var got C.uint64_t
+				atomic.AddUint64(&fdRouteReads, 1)
 				rc := C.writer_read_fd(gw.w, C.int(f.Fd()), C.uint64_t(pos), C.uint64_t(math.MaxUint64), &got)
 				if _, err := f.Seek(pos+int64(got), io.SeekStart); err != nil && rc == 0 {
 					return int64(got), err

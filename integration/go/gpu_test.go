@@ -1,0 +1,58 @@
+//go:build glfsgpu
+
+// Tests of the GPU Writer's io.Copy fast paths.  Goes to bigblob/gpu_test.go
+// of blobcache/glfs next to gpu.go; run with `go test -tags glfsgpu
+// ./bigblob/` on a machine with a GPU and libglfsx.
+
+package bigblob
+
+import (
+	"bytes"
+	"context"
+	"io"
+	"math/rand"
+	"os"
+	"path/filepath"
+	"sync/atomic"
+	"testing"
+
+	"blobcache.io/blobcache/src/blobcache"
+	"blobcache.io/blobcache/src/schema"
+	"github.com/stretchr/testify/require"
+)
+
+// io.Copy(w, f) with an *os.File source reaches gpuWriter.ReadFrom through
+// f.WriteTo's fileWithoutWriteTo wrapper (Go >= 1.22): the pread route must
+// still be taken, and the root must be the one the plain Write route gives.
+func TestCreateFromFileTakesFdRoute(t *testing.T) {
+	if gpuDeviceCount() == 0 {
+		t.Skip("no GPU")
+	}
+	ctx := context.Background()
+	const maxSize = 1 << 20
+	data := make([]byte, 5*maxSize+333)
+	rand.New(rand.NewSource(1)).Read(data)
+	p := filepath.Join(t.TempDir(), "blob")
+	require.NoError(t, os.WriteFile(p, data, 0o600))
+
+	ag := NewMachine()
+	want, err := ag.Create(ctx, schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize),
+		nil, bytes.NewReader(data))
+	require.NoError(t, err)
+
+	f, err := os.Open(p)
+	require.NoError(t, err)
+	defer f.Close()
+	_, err = f.Seek(0, io.SeekStart)
+	require.NoError(t, err)
+	before := atomic.LoadUint64(&fdRouteReads)
+	got, err := ag.Create(ctx, schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize),
+		nil, f)
+	require.NoError(t, err)
+	require.Equal(t, before+1, atomic.LoadUint64(&fdRouteReads), "pread route not taken")
+	require.Equal(t, want.Ref, got.Ref)
+	require.Equal(t, uint64(len(data)), got.Size)
+	pos, err := f.Seek(0, io.SeekCurrent)
+	require.NoError(t, err)
+	require.Equal(t, int64(len(data)), pos) // io.Copy leaves the file at its end
+}

@@ -65,6 +65,57 @@ def test_no_cpu_fallback_without_gpu():
         bigblob.Machine(1024).create(bigblob.MemStore(1024), None, b"abc")
 
 
+def test_library_reads_only_the_documented_knobs():
+    """the library reads five GLFSX_* variables, all
+    tuning (tests/test_gpu_knobs.py runs each at a non-default value); every
+    getenv in its sources names one of them."""
+    knobs = {"GLFSX_BATCH_MIB", "GLFSX_SLOTS", "GLFSX_SPIN_US", "GLFSX_NUMA",
+             "GLFSX_READ_THREADS"}
+    csrc = os.path.join(ROOT, "glfs_amd", "csrc")
+    names, calls = set(), 0
+    for f in os.listdir(csrc):
+        if f.endswith((".cpp", ".hip", ".h")):
+            src = open(os.path.join(csrc, f)).read()
+            names |= set(re.findall(r'getenv\("(GLFSX_\w+)"\)', src))
+            calls += src.count("getenv(")
+    assert names == knobs, names ^ knobs
+    assert calls == len(knobs)
+
+
+def test_file_route_only_for_plain_files(tmp_path):
+    """Writer.read_from takes the parallel pread route only for a plain file
+    (io.FileIO, or a buffered reader over one): a gzip / bz2 / lzma file
+    reports the compressed file's descriptor but a decompressed position, so
+    it must go through readinto."""
+    import bz2
+    import gzip
+    import io
+    import lzma
+    from glfs_amd.bigblob import _regular_fd
+    p = tmp_path / "f.bin"
+    p.write_bytes(b"x" * 1000)
+    with open(p, "rb") as f:
+        assert _regular_fd(f) == f.fileno()
+    with open(p, "rb", buffering=0) as f:
+        assert _regular_fd(f) == f.fileno()
+    with open(p, "r+b") as f:
+        assert _regular_fd(f) == f.fileno()
+    for opener, name in ((gzip.open, "f.gz"), (bz2.open, "f.bz2"), (lzma.open, "f.xz")):
+        q = tmp_path / name
+        with opener(q, "wb") as f:
+            f.write(b"y" * 5000)
+        with opener(q, "rb") as f:
+            assert _regular_fd(f) is None, name
+    assert _regular_fd(io.BytesIO(b"abc")) is None
+    r, w = os.pipe()
+    try:
+        with os.fdopen(r, "rb", closefd=False) as f:
+            assert _regular_fd(f) is None
+    finally:
+        os.close(r)
+        os.close(w)
+
+
 def test_writer_panics_mirror_reference():
     """blob.go:90-95 panics surface as Panic, before any device work."""
     from glfs_amd import _native, bigblob

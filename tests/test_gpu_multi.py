@@ -202,3 +202,35 @@ def test_create_devices_rejects_unaligned_parts(gpu):
         (ctypes.c_void_p * 2)(t.data_ptr(), t.data_ptr() + 4 * MIB),
         (ctypes.c_uint64 * 2)(4 * MIB - 4096, 4 * MIB), None, None, ctypes.byref(root), None)
     assert rc == N.GLFSX_E_ARG
+
+
+def test_create_devices_config5_level_structure(gpu, O):
+    """BASELINE config 5's level structure on the one GPU (VERDICT r4 next
+    #1; bigblob/blob.go:165-206): 8 parts x 16 GiB at 1 MiB blocks, device 0
+    named 8 times (8 PartWorkers, each posting its 16384 data blocks and its
+    one level-1 node), ctext not written -- 131072 blocks -> 8 level-1 refs
+    gathered on the host -> the root node.  The root must equal
+    glfsx_create_device over the same 128 GiB, the first and the last part's
+    level-1 refs the oracle's, and the Posts n0 + 8 + 1."""
+    import torch
+    N = gpu
+    bs, part, nparts = MIB, 16 * GIB, 8
+    total = nparts * part
+    t = torch.empty(total, dtype=torch.uint8, device="cuda")
+    N.check(N.lib.glfsx_fill_splitmix_device(t.data_ptr(), 0, total, 5, None))
+    torch.cuda.synchronize()
+    whole, wposts = N.glfsx_root(), ctypes.c_uint64()
+    N.check(N.lib.glfsx_create_device(bs, None, None, t.data_ptr(), total, None,
+                                      ctypes.byref(whole), ctypes.byref(wposts), None))
+    n0 = total // bs
+    root, l1, posts = _create_devices(N, bs, [0] * nparts,
+                                      [t.data_ptr() + k * part for k in range(nparts)],
+                                      [part] * nparts, nparts)
+    assert root == bytes(whole.ref)
+    assert posts == n0 + nparts + 1 == wposts.value
+    per = part // bs
+    assert l1[:64] == _oracle_level1(O, t, bs, 0, per)
+    assert l1[-64:] == _oracle_level1(O, t, bs, (nparts - 1) * per, per)
+    # the gathered level-1 refs posted as the root node (blob.go:184-206)
+    idx = O.derive_key(bytes(32), b"index")
+    assert O.post(idx, l1.ljust(bs, b"\0"))[0] == root

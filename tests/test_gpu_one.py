@@ -145,7 +145,6 @@ def test_concurrent_small_creates(gpu, O):
     [t.start() for t in th]
     [t.join() for t in th]
     assert not errors, errors[:5]
-    assert os.environ.get("GLFSX_ONE", "1") != "0"
 
 
 @pytest.mark.parametrize("fail_at", [1, 2, 3, 4, 5])

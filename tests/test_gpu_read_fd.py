@@ -166,6 +166,24 @@ def test_read_at_callback_and_python_file_route(gpu, O, file300):
     assert r2.size == len(data) - 17
 
 
+def test_create_from_gzip_file(gpu, O, tmp_path):
+    """bigblob.Machine.create over gzip.open(path): the blob is the
+    DECOMPRESSED bytes (the reader's readinto), never the compressed file's
+    bytes at the decompressed offset."""
+    import gzip
+    from glfs_amd import bigblob
+    data = O.fill_splitmix(5 * MIB + 77, 8)
+    p = tmp_path / "blob.gz"
+    with gzip.open(p, "wb", compresslevel=1) as f:
+        f.write(data)
+    m = bigblob.Machine(MIB)
+    with gzip.open(p, "rb") as f:
+        f.read(5)                                  # a decompressed position of 5
+        r = m.create(bigblob.MemStore(MIB), None, f)
+    assert r.ref.marshal_binary() == _oracle_post_log(O, data[5:], MIB)[0]
+    assert r.size == len(data) - 5
+
+
 def test_read_at_short_reads_and_strict(gpu, O, file300):
     """A ReaderAt that returns at most 100,003 bytes per call (short reads at
     every piece boundary, as a network-backed io.ReaderAt may) into a strict

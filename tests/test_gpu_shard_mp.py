@@ -136,26 +136,36 @@ def test_sharded_write_across_processes(gpu, O, world, bs, nblocks):
         assert rec["n_gpus"] == 2 and rec["root_cid"] == want_root[:32].hex()
 
 
-def test_bench_one_process_gpus(gpu):
-    """bench.py --gpus 2 without a launcher drives two devices from ONE
-    process (glfsx_create_devices).  With one GPU visible it must refuse
-    (exit 2) unless --rehearse, which names device 0 twice and must print
-    n_gpus 2 and the N = 1 root of the same 32 GiB (parts = the splitmix
-    stream at offsets 0 and 16 GiB, seed 3)."""
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_bench_one_process_gpus(gpu, gpus):
+    """bench.py --gpus N without a launcher drives N devices from ONE
+    process (glfsx_create_devices).  With fewer GPUs visible it must refuse
+    (exit 2) unless --rehearse, which names device 0 N times and must print
+    n_gpus N, rehearsal true and the N = 1 root of the same N x 16 GiB blob
+    (parts = the splitmix stream at offsets k x 16 GiB, seed 3).  N = 8 is
+    BASELINE config 5's level structure (8 level-1 nodes under one root)
+    at 16 GiB per part, ctext off so the 128 GiB fit one GPU's HBM."""
     import torch
-    want_root, t = _whole_root(32 * GIB, MIB, 3)
+    total = gpus * 16 * GIB
+    want_root, t = _whole_root(total, MIB, 3)
     del t
     torch.cuda.empty_cache()
-    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--size-gib", "16",
-            "--steps", "1", "--warmup", "0", "--no-extras"]
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--size-gib",
+            "16", "--steps", "1", "--warmup", "0", "--no-extras"]
+    if gpus > 2:
+        base.append("--no-ctext")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    if torch.cuda.device_count() < 2:
+    rehearsal = torch.cuda.device_count() < gpus
+    if rehearsal:
         p = subprocess.run(base, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
-        assert p.returncode == 2 and "only 1 GPU" in p.stderr, (p.returncode, p.stderr[-2000:])
+        assert p.returncode == 2 and "GPU(s) visible" in p.stderr, (p.returncode,
+                                                                    p.stderr[-2000:])
         base.append("--rehearse")
     p = subprocess.run(base, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert rec["n_gpus"] == 2 and rec["root_cid"] == want_root[:32].hex()
-    assert rec["config"]["blob_bytes"] == 32 * GIB
-    assert len(rec["per_device_ms"]["parts"]) == 2
+    assert rec["n_gpus"] == gpus and rec["root_cid"] == want_root[:32].hex()
+    assert rec["rehearsal"] is rehearsal
+    assert rec["config"]["blob_bytes"] == total
+    assert rec["config"]["posts_per_step"] == total // MIB + gpus + 1
+    assert len(rec["per_device_ms"]["parts"]) == gpus

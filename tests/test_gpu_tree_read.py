@@ -428,8 +428,8 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
 
 @pytest.mark.parametrize("n,tree_bs", [(70_000, 2 * MIB), (3000, 4096), (300, 64 * 1024),
                                        (1, 2 * MIB), (257, 1024),
-                                       # the CID pass in two groups with
-                                       # no / some tree blocks beside the second
+                                       # one tree block at 8 MiB (its ref is
+                                       # the root); 5 blocks + an index node
                                        (20_000, 8 * MIB), (20_000, MIB)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
     """glfsx_post_tree_device (blob hashing, tree lines and the tree blob

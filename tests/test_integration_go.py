@@ -180,3 +180,23 @@ def test_glfs_batch_entry_points_in_both_builds():
                      "func SortTreeEntries(", "func CleanPath(", "func getFileMode(",
                      "TypeBlob = ", "TypeTree = "):
             assert name in ref, name
+
+
+def test_read_from_matches_io_copy_file_wrapper():
+    """since Go 1.22 io.Copy(w, *os.File) reaches ReadFrom with
+    f.WriteTo's fileWithoutWriteTo wrapper, so the pread route matches an
+    interface the wrapper satisfies (Fd, Stat, Seek), never the concrete
+    *os.File; gpu_test.go (glfsgpu tag) checks through io.Copy that the
+    route is taken."""
+    src = _read("gpu.go")
+    body = src[src.index("func (gw *gpuWriter) ReadFrom("):]
+    body = body[:body.index("\n}\n")]
+    assert "r.(*os.File)" not in body
+    assert "r.(osFile)" in body and "atomic.AddUint64(&fdRouteReads, 1)" in body
+    iface = re.search(r"type osFile interface \{([^}]*)\}", src)
+    assert iface and "Fd() uintptr" in iface.group(1) and "io.Seeker" in iface.group(1) \
+        and "Stat() (os.FileInfo, error)" in iface.group(1)
+    test = _read("gpu_test.go")
+    assert test.startswith("//go:build glfsgpu\n") and re.search(r"^package bigblob$", test, re.M)
+    assert "fdRouteReads" in test and "ag.Create(ctx" in test and 'import "C"' not in test
+    assert test.count("{") == test.count("}") and test.count("(") == test.count(")")
