@@ -238,6 +238,7 @@ def main():
         if rank == 0 and world == 1 and args.host_rt_gib > 0:
             out["concat"] = concat_leg(N)
             out["postblob_latency"] = postblob_latency(N)
+            out["postblob_concurrency"] = postblob_concurrency(N)
         if hrt is not None and world > 1:
             hrt["value"] = round(world * hrt["value"], 2)
             hrt["bytes"] *= world
@@ -1339,6 +1340,37 @@ def postblob_latency(N, calls=300):
             "what": "one glfs.PostBlob (glfsx_create, bs 2 MiB, blob type salt, counting "
                     "sink) from one Python thread: staging copy, one-shot GPU post "
                     "(k_one / k_med_*), wait"}
+
+
+def postblob_concurrency(N, ln=4096, plan=((1, 3000), (16, 1500), (64, 600), (256, 200))):
+    """glfs.PostBlob as concurrent Go callers run it (VERDICT r4 next #5;
+    glfsposix.go:49 ParMapErr posts one file per call, machine.go:64): T
+    plain C threads (tools/libpostbench.so; no interpreter between calls),
+    each posting its own distinct 4 KiB blobs one glfsx_create at a time
+    (bs 2 MiB, blob type salt, counting sink).  calls/s = all calls / wall
+    time; the CPU port's per-blob rate on 1 core and on all cores of this
+    job is cpu_baseline.small_blobs (the same 4 KiB posts as a batch, no
+    call overhead)."""
+    from glfs_amd import glfs
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libpostbench.so"))
+    lib.postbench_run.restype = ctypes.c_int
+    lib.postbench_run.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p,
+                                  ctypes.c_int, ctypes.c_void_p]
+    salt = glfs.Machine().make_salt("blob")
+    import torch
+    dev = int(torch.cuda.current_device())
+    res = {}
+    for threads, calls in plan:
+        out = (ctypes.c_double * 5)()
+        rc = lib.postbench_run(threads, ln, calls, salt, dev, out)
+        N.check(rc, "postbench")
+        res[str(threads)] = {"calls_per_s": round(out[0] / out[1]), "calls": int(out[0]),
+                             "p50_us": round(out[2], 1), "p90_us": round(out[3], 1),
+                             "p99_us": round(out[4], 1)}
+    return {"by_threads": res, "blob_bytes": ln,
+            "what": "concurrent glfs.PostBlob of distinct 4 KiB blobs: T C threads each calling "
+                    "glfsx_create back to back (bs 2 MiB, blob type salt, counting sink); "
+                    "calls_per_s = calls / wall time, latency percentiles per call"}
 
 
 def concat_leg(N, bs=MIB, size=GIB):

@@ -118,6 +118,10 @@ struct Ctx {
   hipStream_t stream2 = nullptr;
   std::vector<hipEvent_t> events;
   PinBuf h_tree;
+  // its tree items (TreeItems: the struct, then its counters and CVs) and
+  // their timeout word
+  DevBuf d_titems;
+  PinBuf h_titems, h_terr;
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
@@ -235,31 +239,40 @@ hipStream_t pick_stream(Ctx *c, void *stream) {
 }
 
 // ---- One-shot posts (launch_one) ----
-// A post of one message of at most kMaxOneLen bytes from host memory: the
+// A post of one message of at most kMaxMedLen bytes from host memory: the
 // bytes sit in pinned staging, the kernel reads them there and writes ctext
-// and ref straight back into pinned staging, so a post is one launch and one
-// wait instead of copy, DEK pass, keystream, CID pass and two copies.
+// and ref straight back into pinned staging, then sets the request's flag
+// (pinned, OneDesc::flag) to the launch's sequence number, so a post is one
+// launch and a wait on a host word -- no stream query.
 // Concurrent callers (glfs.Machine is used from many goroutines) are
-// coalesced, group-commit style: a caller that finds a free launch lane
-// becomes the leader, takes every pending request (one workgroup each) into
-// one launch on that lane, hands the leadership on and waits for its launch;
-// the others wait for their request to be marked done or for the
-// leadership.  Up to kOneLanes launches are in flight, each carrying
-// whatever queued while the earlier ones ran.  Per-caller launches would cap
-// the process at GPU_MAX_HW_QUEUES (4) posts in flight.
+// coalesced, group-commit style: a caller that finds the leadership free
+// and a free launch lane takes every pending request into one launch (one
+// workgroup each) and hands the leadership on at once; every caller then
+// waits for its own flag.  A lane is free again once its launch has
+// completed (its descriptors and flags are read and written until then):
+// up to kOneLanes launches are in flight, each carrying whatever queued
+// while the earlier ones ran.
 constexpr uint32_t kOneBatch = 1024;
-constexpr int kOneLanes = 4;
+constexpr int kOneLanes = 8;
+struct OneLane;
 struct OneReq {
   OneDesc d{};
-  std::atomic<int> done{0};
+  std::atomic<int> armed{0};  // flag / seq / lane below are set (by the leader)
+  std::atomic<int> done{0};   // failed before launch (rc, err)
+  const uint32_t *flag = nullptr;
+  uint32_t seq = 0;
+  OneLane *lane = nullptr;
   int rc = 0;
   std::string err;
 };
 struct OneLane {
-  std::atomic<bool> busy{false};
+  bool busy = false;          // a launch in flight (read and written by the leader only)
   hipStream_t s = nullptr;
+  hipEvent_t ev = nullptr;    // recorded after the launch
+  uint32_t seq = 0;           // the last launch's sequence number
   OneDesc *h_desc = nullptr;  // pinned, kOneBatch descriptors
   OneDesc *d_desc = nullptr;  // the kernel's view of h_desc
+  uint32_t *h_flag = nullptr, *d_flag = nullptr;  // pinned, kOneBatch flags
   // medium posts: device copies of the messages, and per descriptor
   // kMedAuxWords words of CVs / arrival counter / DEK (zeroed when grown;
   // the kernels leave every counter at zero)
@@ -288,20 +301,29 @@ int poster_get(int dev, OnePoster **out) {
   auto *p = new OnePoster();
   p->dev = dev;
   for (OneLane &l : p->lane) {
-    void *h = nullptr, *d = nullptr;
+    void *h = nullptr, *d = nullptr, *hf = nullptr, *df = nullptr;
     if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&l.ev, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&h, sizeof(OneDesc) * kOneBatch, hipHostMallocDefault) != hipSuccess ||
-        hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
+        hipHostMalloc(&hf, sizeof(uint32_t) * kOneBatch, hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&df, hf, 0) != hipSuccess) {
       for (OneLane &x : p->lane) {
         if (x.h_desc) (void)hipHostFree(x.h_desc);
+        if (x.h_flag) (void)hipHostFree(x.h_flag);
         if (x.s) (void)hipStreamDestroy(x.s);
+        if (x.ev) (void)hipEventDestroy(x.ev);
       }
-      if (h) (void)hipHostFree(h);
+      if (h && h != static_cast<void *>(l.h_desc)) (void)hipHostFree(h);
+      if (hf) (void)hipHostFree(hf);
       delete p;
       return fail(GLFSX_E_DEVICE, "one-shot post setup failed on device %d", dev);
     }
     l.h_desc = static_cast<OneDesc *>(h);
     l.d_desc = static_cast<OneDesc *>(d);
+    l.h_flag = static_cast<uint32_t *>(hf);
+    l.d_flag = static_cast<uint32_t *>(df);
+    memset(hf, 0, sizeof(uint32_t) * kOneBatch);
   }
   g_posters.push_back(p);
   *out = p;
@@ -309,8 +331,9 @@ int poster_get(int dev, OnePoster **out) {
 }
 
 // One launch of k_one over the batch's small messages and one launch_med
-// (two kernels) over its medium ones, on the lane's stream.
-int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
+// (two kernels) over its medium ones, on the lane's stream; request i's
+// flag is lane.h_flag[i], set to `seq` when its results are in place.
+int one_launch(OneLane &L, const std::vector<OneReq *> &batch, uint32_t seq) {
   uint64_t max_small = 0, max_med = 0, med_bytes = 0;
   size_t ns = 0, nm = 0;
   for (const OneReq *r : batch) {
@@ -333,12 +356,15 @@ int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
   }
   size_t is = 0, im = ns;
   uint64_t mo = 0;
-  for (const OneReq *r : batch) {
+  for (size_t k = 0; k < batch.size(); ++k) {
+    const OneReq *r = batch[k];
+    OneDesc d = r->d;
+    d.flag = L.d_flag + k;
+    d.seq = seq;
     if (r->d.len <= kMaxOneLen) {
-      L.h_desc[is++] = r->d;
+      L.h_desc[is++] = d;
       continue;
     }
-    OneDesc d = r->d;
     uint32_t *aux = reinterpret_cast<uint32_t *>(L.med_aux.p) + (im - ns) * kMedAuxWords;
     d.dmsg = L.med_msg.u8() + mo;
     d.cvs = aux;
@@ -349,11 +375,17 @@ int one_launch(OneLane &L, const std::vector<OneReq *> &batch) {
   }
   if (ns) HIP_TRY(launch_one(L.d_desc, uint32_t(ns), max_small, L.s));
   if (nm) HIP_TRY(launch_med(L.d_desc + ns, uint32_t(nm), max_med, L.s));
+  HIP_TRY(hipEventRecord(L.ev, L.s));
   return 0;
 }
 
-// Post r on device dev (the calling thread's current device); returns when
-// r's ctext and ref are in its staging.
+// Request r has its results: its flag reached its launch's sequence number.
+bool one_finished(const OneReq *r) {
+  if (!r->armed.load(std::memory_order_acquire)) return false;
+  const uint32_t v = __atomic_load_n(r->flag, __ATOMIC_ACQUIRE);
+  return int32_t(v - r->seq) >= 0;
+}
+
 // Post rs[0..n) on device dev (the calling thread's current device); returns
 // when every request's ctext and ref are in its staging.
 int one_post_many(int dev, OneReq *const *rs, size_t n) {
@@ -366,9 +398,11 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
     std::lock_guard<std::mutex> lk(P->mu);
     P->pending.insert(P->pending.end(), rs, rs + n);
   }
-  size_t ndone = 0;  // rs[0..ndone) are done
+  size_t ndone = 0;  // rs[0..ndone) are finished or failed
   for (uint32_t spins = 0;; ++spins) {
-    while (ndone < n && rs[ndone]->done.load(std::memory_order_acquire)) ++ndone;
+    while (ndone < n && (rs[ndone]->done.load(std::memory_order_acquire) ||
+                         one_finished(rs[ndone])))
+      ++ndone;
     if (ndone == n) {
       for (size_t i = 0; i < n; ++i)
         if (rs[i]->rc) return fail(rs[i]->rc, "%s", rs[i]->err.c_str());
@@ -376,13 +410,19 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
     }
     bool idle = false;
     if (P->leader.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
+      // a lane whose last launch has completed
       OneLane *L = nullptr;
+      int rc = 0;
       for (OneLane &l : P->lane) {
-        bool b = false;
-        if (l.busy.compare_exchange_strong(b, true, std::memory_order_acq_rel)) {
-          L = &l;
-          break;
+        if (l.busy) {
+          const hipError_t q = hipEventQuery(l.ev);
+          if (q == hipErrorNotReady) continue;
+          if (q != hipSuccess && !rc)
+            rc = fail(GLFSX_E_DEVICE, "one-shot post: %s", hipGetErrorString(q));
+          l.busy = false;
         }
+        L = &l;
+        break;
       }
       std::vector<OneReq *> batch;
       if (L) {
@@ -402,34 +442,51 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         batch.assign(P->pending.begin(), P->pending.begin() + k);
         P->pending.erase(P->pending.begin(), P->pending.begin() + k);
       }
-      int rc = 0;
-      if (!batch.empty()) rc = one_launch(*L, batch);
-      // the next batch may launch on another lane while this one runs
-      P->leader.store(false, std::memory_order_release);
-      if (L) {
-        // wait even after a failed launch: an earlier kernel of the batch may
-        // still be writing the requests' staging, which their owners reuse
-        // as soon as done is set
-        if (!batch.empty()) {
-          const hipError_t e = stream_wait(L->s);
-          if (e != hipSuccess && !rc)
-            rc = fail(GLFSX_E_DEVICE, "one-shot post: %s", hipGetErrorString(e));
-        }
-        L->busy.store(false, std::memory_order_release);
-        const std::string msg = rc ? tls_err : std::string();
-        // a request's owner may return (and free it) once done is set
-        for (OneReq *b : batch) {
-          b->rc = rc;
-          b->err = msg;
-          b->done.store(1, std::memory_order_release);
+      if (!batch.empty()) {
+        const uint32_t seq = ++L->seq;
+        if (!rc) rc = one_launch(*L, batch, seq);
+        if (!rc) {
+          L->busy = true;
+          for (size_t k = 0; k < batch.size(); ++k) {
+            batch[k]->flag = L->h_flag + k;
+            batch[k]->seq = seq;
+            batch[k]->lane = L;
+            batch[k]->armed.store(1, std::memory_order_release);
+          }
+        } else {
+          // nothing of this batch runs: its owners get the error (a
+          // request's owner may return, and free it, once done is set)
+          (void)hipStreamSynchronize(L->s);
+          const std::string msg = tls_err;
+          for (OneReq *b : batch) {
+            b->rc = rc;
+            b->err = msg;
+            b->done.store(1, std::memory_order_release);
+          }
         }
       }
+      P->leader.store(false, std::memory_order_release);
       continue;
     }
-    if (spins < 20000)
+    if (spins < 20000) {
       sched_yield();
-    else
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      continue;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (spins % 1024 == 0) {
+      // a long wait: a launch that failed on the device never sets its flags
+      for (size_t i = ndone; i < n; ++i) {
+        const OneReq *r = rs[i];
+        if (!r->armed.load(std::memory_order_acquire) || one_finished(r)) continue;
+        // (the lane's event is ours or a later launch's: either way ours
+        // has completed when it has)
+        const hipError_t q = hipEventQuery(r->lane->ev);
+        if (q == hipErrorNotReady || one_finished(r)) continue;
+        return fail(GLFSX_E_DEVICE, "one-shot post: %s",
+                    q == hipSuccess ? "the launch completed without its result flag"
+                                    : hipGetErrorString(q));
+      }
+    }
   }
 }
 
@@ -553,11 +610,21 @@ std::vector<SaltCacheEntry> g_salts;
 int derive_salts(Ctx *c, const uint8_t *salt, Salts *s) {
   static const uint8_t zero[32] = {0};
   const uint8_t *sl = salt ? salt : zero;
+  // the calling thread's last salt first: concurrent PostBlob callers (one
+  // salt per type) never touch the process-wide lock
+  thread_local SaltCacheEntry last{};
+  thread_local bool have_last = false;
+  if (have_last && memcmp(last.salt, sl, 32) == 0) {
+    *s = last.s;
+    return 0;
+  }
   {
     std::lock_guard<std::mutex> lk(g_salts_mu);
     for (const auto &e : g_salts)
       if (memcmp(e.salt, sl, 32) == 0) {
         *s = e.s;
+        last = e;
+        have_last = true;
         return 0;
       }
   }
@@ -566,6 +633,8 @@ int derive_salts(Ctx *c, const uint8_t *salt, Salts *s) {
   SaltCacheEntry ent;
   memcpy(ent.salt, sl, 32);
   ent.s = *s;
+  last = ent;
+  have_last = true;
   std::lock_guard<std::mutex> lk(g_salts_mu);
   if (g_salts.size() >= 64) g_salts.erase(g_salts.begin());
   g_salts.push_back(ent);
@@ -2125,9 +2194,52 @@ void glfsx_writer_free(glfsx_writer *w) {
   delete w;
 }
 
+namespace {
+// glfsx_create of a blob of at most one block of <= kMaxMedLen bytes (a
+// glfs.PostBlob of a small file, machine.go:64): its Writer would stage the
+// bytes, post them as the tail block at Finish and return that block's ref
+// as the root (blob.go:136-140, 190-193) -- or, for the empty blob, post
+// the empty index node (blob.go:187-189).  The same single Post, without a
+// Writer: the thread's pinned one-shot staging and one coalesced one-shot
+// post (no writer pools, locks or streams per call).
+int create_one_block(Ctx *c, uint64_t bs, const uint8_t *salt, const uint8_t *cid_key,
+                     const void *data, uint64_t size, glfsx_post_fn post, void *post_ctx,
+                     glfsx_root *out) {
+  Salts salts;
+  if (int e = derive_salts(c, salt, &salts)) return e;
+  if (int e = c->h_oin.ensure(size + 64)) return e;
+  if (int e = c->h_oct.ensure(size + 64)) return e;
+  if (int e = c->h_oref.ensure(64)) return e;
+  if (size) par_memcpy(c->h_oin.u8(), static_cast<const uint8_t *>(data), size);
+  OneReq r;
+  r.d.src = c->h_oin.dptr();
+  r.d.ctext = post ? c->h_oct.dptr() : nullptr;
+  r.d.ref = c->h_oref.dptr();
+  r.d.len = uint32_t(size);
+  r.d.present = uint32_t(size);
+  one_keys(r.d, size ? salts.raw : salts.index, cid_key);
+  if (int e = one_post(c->dev, &r)) return e;
+  memcpy(out->ref, c->h_oref.p, 64);
+  out->size = size;
+  out->block_size = bs;
+  if (post) {
+    const int rc = post(post_ctx, size ? 0 : 1, out->ref, c->h_oct.p, size);
+    if (rc) return fail(GLFSX_E_STORE, "store.Post failed with code %d", rc);
+  }
+  return 0;
+}
+}  // namespace
+
 int glfsx_create(uint64_t block_size, uint64_t store_max, const uint8_t *salt,
                  const uint8_t *cid_key, const void *data, uint64_t size,
                  glfsx_post_fn post, void *post_ctx, glfsx_root *out) {
+  const uint64_t bs = block_size ? block_size : store_max;  // blob.go:86-89
+  if (out && (size == 0 || data) && bs <= store_max && bs >= GLFSX_MIN_BLOCK_SIZE &&
+      bs <= kMaxMsgLen && size <= bs && size <= kMaxMedLen) {
+    Ctx *c;
+    if (int e = ctx_get(&c)) return e;
+    return create_one_block(c, bs, salt, cid_key, data, size, post, post_ctx, out);
+  }
   int err = 0;
   glfsx_writer *w =
       glfsx_writer_new(block_size, store_max, salt, cid_key, post, post_ctx, &err);
@@ -3001,6 +3113,27 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   } else {
     blake3_iv_words(sj.cid_key);
   }
+  // The tree blob's blocks as work items of the blobs' CID pass (TreeItems):
+  // tree blocks of whole 64 KiB spans, at most 64 per block, 16-B aligned
+  // buffers (else, or when repeating a failed call, the tree blob is posted
+  // after the CID pass).  Counters and flags are zeroed on B before the
+  // layout, sized for the line buffer's capacity.
+  const bool items = tls_fused && tree_bs % kTreeSpan == 0 && tree_bs / kTreeSpan <= 64 &&
+                     ((reinterpret_cast<uintptr_t>(d_lines) |
+                       reinterpret_cast<uintptr_t>(d_tree_ctext)) & 15) == 0;
+  const uint64_t spans_max = (lines_cap + kTreeSpan - 1) / kTreeSpan;
+  const uint64_t blk_max = (lines_cap + tree_bs - 1) / tree_bs;
+  // words after the struct: done[wgs], dek_cnt / cid_cnt / ready[blk_max],
+  // then the CVs (2 x 8 words per span)
+  const uint64_t ti_hdr = (sizeof(TreeItems) + 255) / 256 * 256;
+  const uint64_t ti_zero = 4 * (wgs + 3 * blk_max);
+  if (items) {
+    if (int e = c->d_titems.ensure(ti_hdr + ti_zero + 64 * spans_max + 64)) return e;
+    if (int e = c->h_titems.ensure(sizeof(TreeItems))) return e;
+    if (int e = c->h_terr.ensure(64)) return e;
+    __atomic_store_n(reinterpret_cast<uint32_t *>(c->h_terr.p), 0u, __ATOMIC_RELAXED);
+    HIP_TRY(hipMemsetAsync(c->d_titems.u8() + ti_hdr, 0, ti_zero, B));
+  }
   sj.passes = 1;  // the DEK pass: the critical path, queued first
   HIP_TRY(launch_post_small(sj, A));
   HIP_TRY(launch_tree_layout(tj, B));
@@ -3011,7 +3144,8 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   sj.hex_out = static_cast<uint8_t *>(d_lines);
   sj.hex_pos = tj.hex_pos;
   sj.cid_wait = ev_static;
-  HIP_TRY(launch_post_small(sj, A));
+  if (!items) HIP_TRY(launch_post_small(sj, A));
+  // the layout (beside the DEK pass) gives the tree blob's size
   HIP_TRY(hipEventSynchronize(ev_layout));
   const uint64_t total = static_cast<const uint64_t *>(c->h_tree.p)[wgs];
   if (total > lines_cap) {
@@ -3020,22 +3154,63 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
                 (unsigned long long)total, (unsigned long long)lines_cap);
   }
-  // the tree blob, on A after the CID pass (its lines are complete then)
   const uint64_t nblk = (total + tree_bs - 1) / tree_bs;
   const uint64_t n1 = (nblk + tree_bs / 64 - 1) / (tree_bs / 64);
   if (int e = level_prepare(c->d_lvl_a, nblk, n1, tree_bs, A)) return e;
   uint8_t *lvl = c->d_lvl_a.u8();
-  PostJob j{};
-  j.src = static_cast<const uint8_t *>(d_lines);
-  j.ctext = static_cast<uint8_t *>(d_tree_ctext);
-  j.stride = tree_bs;
-  j.msg_len = tree_bs;
-  j.n = nblk;
-  j.last_len = total - (nblk - 1) * tree_bs;
-  j.out = RefLayout{lvl, ~0ull, 0};  // ref t at byte 64t
-  words_from_key(j.salt, tsalts.raw);
-  cid_words(j, cid_key);
-  HIP_TRY(launch_post(j, A, tls_fused));
+  if (items) {
+    // the blobs' CID pass with the tree blob's items behind them
+    TreeItems &T = *static_cast<TreeItems *>(c->h_titems.p);
+    T = TreeItems{};
+    uint32_t *z = reinterpret_cast<uint32_t *>(c->d_titems.u8() + ti_hdr);
+    T.lines = static_cast<const uint8_t *>(d_lines);
+    T.ctext = static_cast<uint8_t *>(d_tree_ctext);
+    T.refs = lvl;
+    T.total = total;
+    T.bs = tree_bs;
+    T.spans = uint32_t((total + kTreeSpan - 1) / kTreeSpan);
+    T.spb = uint32_t(tree_bs / kTreeSpan);
+    T.n = uint32_t(n);
+    T.wgs = uint32_t(wgs);
+    T.wg_prefix = tj.scratch + n;  // then the total (k_tree_prefix)
+    T.done = z;
+    T.dek_cnt = z + wgs;
+    T.cid_cnt = T.dek_cnt + blk_max;
+    T.ready = T.cid_cnt + blk_max;
+    T.dek_cv = T.ready + blk_max;
+    T.cid_cv = T.dek_cv + 8 * spans_max;
+    T.err = reinterpret_cast<uint32_t *>(c->h_terr.dptr());
+    T.wait_ticks = 100000000ull;  // 1 s of s_memrealtime
+    words_from_key(T.salt, tsalts.raw);
+    memcpy(T.cid_key, sj.cid_key, 32);
+    T.cid_base = sj.cid_keyed ? 16u : 0u;  // KEYED_HASH
+    HIP_TRY(hipMemcpyAsync(c->d_titems.p, &T, sizeof T, hipMemcpyHostToDevice, A));
+    sj.tree = reinterpret_cast<const TreeItems *>(c->d_titems.p);
+    sj.tree_items = 2ull * T.spans;
+    HIP_TRY(launch_post_small(sj, A));
+  } else {
+    // the tree blob, on A after the CID pass (its lines are complete then)
+    PostJob j{};
+    j.src = static_cast<const uint8_t *>(d_lines);
+    j.ctext = static_cast<uint8_t *>(d_tree_ctext);
+    j.stride = tree_bs;
+    j.msg_len = tree_bs;
+    j.n = nblk;
+    j.last_len = total - (nblk - 1) * tree_bs;
+    j.out = RefLayout{lvl, ~0ull, 0};  // ref t at byte 64t
+    words_from_key(j.salt, tsalts.raw);
+    cid_words(j, cid_key);
+    HIP_TRY(launch_post(j, A, tls_fused));
+  }
+  // a tree item that gave up waiting invalidates the call: repeated with
+  // the tree blob posted after the CID pass (with_fused_retry)
+  auto items_check = [&]() -> int {
+    if (items && __atomic_load_n(reinterpret_cast<uint32_t *>(c->h_terr.p), __ATOMIC_ACQUIRE)) {
+      tls_fused_failed = true;
+      return fail(GLFSX_E_DEVICE, "a tree item's wait timed out; its results were discarded");
+    }
+    return 0;
+  };
   *lines_len = total;
   tree_root->size = total;
   tree_root->block_size = tree_bs;
@@ -3044,11 +3219,15 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, A));
     HIP_TRY(stream_wait(A));  // (B is drained: A waited for its static lines)
     if (int e = fused_check(A)) return e;
+    if (int e = items_check()) return e;
     memcpy(tree_root->ref, c->h_root.p, 64);
     return 0;
   }
   uint64_t posts = 0;
-  return build_up(c, A, tsalts, cid_key, tree_bs, lvl, n1, &c->d_lvl_b, tree_root->ref, &posts);
+  if (int e = build_up(c, A, tsalts, cid_key, tree_bs, lvl, n1, &c->d_lvl_b, tree_root->ref,
+                       &posts))
+    return e;
+  return items_check();
 }
 }  // namespace
 

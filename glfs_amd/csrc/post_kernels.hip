@@ -714,12 +714,17 @@ __device__ __forceinline__ void pair_pipelined(
 // next even block's before the odd one, so HBM latency is covered and no
 // buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
 // the chaining-value reset are per-chunk (scalar), not per-block selects.
-template <int G, bool CHACHA, bool STAGE = false, int A = 2>
+// LAUX: cache policy of the staged loads (kLoadCoherent: device-coherent,
+// for bytes other XCDs wrote during the launch).  cst: bytes the staged
+// ctext stores may write from cmsg (0: none -- the stores fall outside the
+// buffer descriptor and are dropped; default: clen).
+constexpr uint32_t kLoadCoherent = 16;  // SC1 (gfx950 cache policy bits)
+template <int G, bool CHACHA, bool STAGE = false, int A = 2, uint32_t LAUX = 0>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
     const uint32_t (&dek)[8], uint32_t sbase = 0, uint32_t clen = 0,
-    uint32_t cbase = 0) {
+    uint32_t cbase = 0, uint32_t cst = ~0u) {
   constexpr int D = ilog2(G);
   constexpr uint32_t NB = 16u * G;
   uint32_t stk[D > 0 ? D : 1][8];
@@ -751,7 +756,8 @@ __device__ __forceinline__ void lane_subtree_full(
   const uint32_t vo = ((first + (r - l) * uint32_t(G)) << 10) + (pc << 4);
   // wave-uniform descriptors (msg / cmsg, clen uniform over the wave)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      CHACHA ? cmsg : const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
+      CHACHA ? cmsg : const_cast<uint8_t *>(msg), 0, STAGE ? (cst == ~0u ? clen : cst) : 0u,
+      0x00020000);
   const __amdgpu_buffer_rsrc_t rsrc_ld = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t *>(msg), 0, STAGE ? clen : 0u, 0x00020000);
   const uint32_t sb = __builtin_amdgcn_readfirstlane(sbase);
@@ -763,7 +769,7 @@ __device__ __forceinline__ void lane_subtree_full(
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc_ld, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
           16, (k & 1) ? (lo0 ^ 64u) : lo0, ((8u * k * uint32_t(G)) << 10) + 128u * s,
-          0, 0);
+          0, LAUX);
   };
   if constexpr (gl) issue(0);
   for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
@@ -1782,6 +1788,17 @@ __device__ __forceinline__ void one_store(const uint4 *img_u4, uint8_t *dst, uin
   }
 }
 
+// The post's results (ctext, ref) are in the caller's staging: every lane's
+// stores are done, then one release store of the descriptor's sequence
+// number into its flag (pinned host memory) tells the waiting caller, with
+// no stream query (OneDesc::flag; nullable).
+__device__ __forceinline__ void one_signal(const OneDesc *dp) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && dp->flag)
+    __hip_atomic_store(dp->flag, dp->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <int QUADS>
 __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
   __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
@@ -1824,6 +1841,7 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
     r[8 + q] = dek[q];
     r[12 + q] = dek[4 + q];
   }
+  one_signal(dp);
 }
 
 // ---- Medium one-shot posts (kMaxOneLen < len <= kMaxMedLen) ----
@@ -1928,6 +1946,10 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
   const uint32_t base = dp->cid_keyed ? kKeyed : 0u;
   uint32_t cl, ch;
   one_hash(cl, ch, img, ts, passbuf, slen, ckey, base, q, quad, rel, sidx << 6, false);
+  // this span's ctext stores are done before it counts in (the last
+  // workgroup signals the caller)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   bool last;
   med_publish_merge(cl, ch, dp, sidx, W, ts, passbuf, &s_flag, ckey, base, q, quad, rel,
                     &last);
@@ -1936,6 +1958,7 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
     r[q] = cl;
     r[4 + q] = ch;
   }
+  if (last) one_signal(dp);
 }
 
 // Small blobs (glfs.PostBlob of many blobs that each fit one bigblob block,
@@ -1959,6 +1982,10 @@ struct SArgs {
   uint64_t small_max;  // longer blobs are skipped (SmallJob::small_max)
   uint8_t *hex_out;    // CID pass, nullable: the root as tree-line hex digits
   const uint64_t *hex_pos;
+  // CID pass of the one-call tree route: the tree blob's work items after
+  // the blobs' (TreeItems, device memory; nullptr and 0 otherwise)
+  const TreeItems *tree;
+  uint64_t tree_items;
 };
 
 // Lower-case hex digits of bytes 0 and 1 of x, in output order (hi(b0)
@@ -1974,7 +2001,10 @@ __device__ __forceinline__ uint32_t hex4(uint32_t x) {
 // of a TreeEntry line, encoding as tree_kernels.hip's hex32) at dst, any
 // alignment: aligned 4-byte stores of the digits shifted into place
 // (alignbyte), the two partial words at the ends byte by byte -- no byte
-// outside [dst, dst + 64) is written.
+// outside [dst, dst + 64) is written.  COH: device-coherent (agent-scope
+// atomic) stores, for lines that tree items on other XCDs read in the same
+// launch.
+template <bool COH = false>
 __device__ __forceinline__ void put_hex32(uint8_t *dst, const uint32_t w[8]) {
   const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(dst) & 3u);
   const uint32_t sh = 8u * (4u - s);  // s = 0: the whole next word
@@ -1985,11 +2015,20 @@ __device__ __forceinline__ void put_hex32(uint8_t *dst, const uint32_t w[8]) {
     const uint32_t cur = k < 16 ? hex4(w[k >> 1] >> (16 * (k & 1))) : 0u;
     const uint32_t v = uint32_t(((uint64_t(cur) << 32) | prev) >> sh);
     if ((k >= 1 && k <= 15) || (k == 0 && s == 0)) {
-      base[k] = v;
+      if constexpr (COH)
+        __hip_atomic_store(base + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        base[k] = v;
     } else {
       const uint32_t lo = k == 0 ? s : 0u, hi = k == 0 ? 4u : s;
       uint8_t *b = reinterpret_cast<uint8_t *>(base + k);
-      for (uint32_t x = lo; x < hi; ++x) b[x] = uint8_t(v >> (8u * x));
+      for (uint32_t x = lo; x < hi; ++x) {
+        if constexpr (COH)
+          __hip_atomic_store(b + x, uint8_t(v >> (8u * x)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          b[x] = uint8_t(v >> (8u * x));
+      }
     }
     prev = cur;
   }
@@ -2049,8 +2088,13 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
   if (CHACHA && a.hex_out) {  // the tree line's cid and dek digits
     const uint64_t pos = a.hex_pos[i];
     if (pos != ~0ull) {  // ~0: the lines did not fit their buffer
-      put_hex32(a.hex_out + pos, cv);
-      put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+      if (a.tree) {
+        put_hex32<true>(a.hex_out + pos, cv);
+        put_hex32<true>(a.hex_out + pos + kDekAfterCid, dek);
+      } else {
+        put_hex32(a.hex_out + pos, cv);
+        put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+      }
     }
   }
 }
@@ -2116,10 +2160,229 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
     if (CHACHA && a.hex_out) {
       const uint64_t pos = a.hex_pos[i];
       if (pos != ~0ull) {
-        put_hex32(a.hex_out + pos, cv);
-        put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+        if (a.tree) {
+          put_hex32<true>(a.hex_out + pos, cv);
+          put_hex32<true>(a.hex_out + pos + kDekAfterCid, dek);
+        } else {
+          put_hex32(a.hex_out + pos, cv);
+          put_hex32(a.hex_out + pos + kDekAfterCid, dek);
+        }
       }
     }
+  }
+}
+
+// ---- Tree items: the one-call config-4 route's tree blob (TreeItems) ----
+// Left-complete merge of the CVs of lanes [0, cnt) of the wave (lane l =
+// leaf l, cnt <= 64, uniform), ROOT on the top parent when `root`; the
+// result is in lane 0.  At stride st, lane l (l % 2st == 0) takes lane
+// l + st as its right child when that leaf exists, else passes through:
+// BLAKE3's tree (as tree_reduce).
+template <int A>
+__device__ __forceinline__ void wave_merge(uint32_t (&cv)[8], uint32_t cnt, bool root,
+                                           const uint32_t (&key)[8], uint32_t base) {
+  const uint32_t l = threadIdx.x & 63u;
+  for (uint32_t st = 1; st < cnt; st <<= 1) {
+    uint32_t m[16];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      m[w] = cv[w];
+      m[8 + w] = uint32_t(__shfl_down(int(cv[w]), st, 64));
+    }
+    if ((l & (2 * st - 1)) == 0 && l + st < cnt) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cv[w] = key[w];
+      b3_compress<A>(cv, m, 0u, 0u, 64u,
+                     base | kParent | ((root && 2 * st >= cnt) ? kRoot : 0u));
+    }
+  }
+}
+
+// Device-coherent loads of bytes other XCDs wrote during the launch (the
+// tree lines' hex digits: put_hex32<true>): agent-scope atomic loads,
+// which do not return a stale line of this XCD's L2.
+__device__ __forceinline__ uint32_t coh_word(const uint8_t *p, uint32_t avail) {
+  if (avail >= 4)
+    return __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t w = 0;
+  for (uint32_t b = 0; b < avail; ++b)
+    w |= uint32_t(__hip_atomic_load(p + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+         << (8 * b);
+  return w;
+}
+
+// One chunk of clen (<= 1024) bytes at p (4-B aligned), chunk counter
+// `chunk`, through device-coherent loads: the tree items' partial span (the
+// blob's last).  CHACHA: the keystream of dek XORed in first, the ctext
+// stored at cp (nullable).  root: the chunk is the whole message.
+template <bool CHACHA>
+__device__ void lane_chunk_coh(uint32_t (&cv)[8], const uint8_t *p, uint8_t *cp, uint32_t clen,
+                               uint32_t chunk, bool root, const uint32_t (&key)[8],
+                               uint32_t base, const uint32_t (&dek)[8]) {
+  const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = key[i];
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t avail = clen - min(clen, 64u * b) < 64u ? clen - min(clen, 64u * b) : 64u;
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      m[i] = uint32_t(4 * i) < avail ? coh_word(p + 64 * b + 4 * i, avail - 4 * i) : 0u;
+    if constexpr (CHACHA) {
+      uint32_t x[16];
+      chacha_block<0>(x, dek, (chunk << 4) + b);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] ^= x[i];
+      if (avail < 64) mask_tail(m, avail);
+      if (cp) store_block<false>(cp + 64 * b, m, avail);
+    }
+    uint32_t fl = base;
+    if (b == 0) fl |= kChunkStart;
+    if (b + 1 == nb) fl |= kChunkEnd | (root ? kRoot : 0u);
+    b3_compress<0>(cv, m, chunk, 0u, avail, fl);
+  }
+}
+
+// Tree item t (of 2 x spans): t < spans = the DEK item of span t, else the
+// CID item of span t - spans.  The whole wave runs it; lane l hashes chunk
+// l of the span.  Waits are bounded by T->wait_ticks (a timeout sets *err;
+// the host then discards the call's results).
+template <int A>
+__device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds_u4) {
+  const TreeItems *T = a.tree;
+  const uint32_t spans = T->spans, spb = T->spb;
+  const bool cid = t >= spans;
+  const uint32_t g = uint32_t(cid ? t - spans : t);
+  const uint32_t b = g / spb, s = g - b * spb;
+  const uint64_t total = T->total;
+  const uint64_t lo = uint64_t(g) * kTreeSpan;
+  const uint32_t slen = uint32_t(min<uint64_t>(kTreeSpan, total - lo));
+  const uint64_t blen = min<uint64_t>(T->bs, total - uint64_t(b) * T->bs);
+  const uint32_t W = uint32_t((blen + kTreeSpan - 1) / kTreeSpan);  // spans of block b
+  const uint32_t C = (slen + 1023) >> 10;                          // chunks of span g
+  const uint32_t l = threadIdx.x & 63u;
+  uint8_t *ref = T->refs + 64ull * b;
+  if (l == 0) {  // the wait: the span's entries (DEK) or the block's DEK (CID)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    if (!cid) {
+      // entry groups whose lines touch [lo, lo + slen): w0 = the group that
+      // holds byte lo, w1 = the one that holds byte lo + slen - 1
+      const uint64_t *P = T->wg_prefix;
+      const uint32_t wgs = T->wgs;
+      uint32_t w0 = 0, w1 = 0;
+      for (uint32_t lo_i = 0, hi_i = wgs; lo_i < hi_i;) {  // last w with P[w] <= lo
+        const uint32_t mid = (lo_i + hi_i) >> 1;
+        if (P[mid] <= lo) { w0 = mid; lo_i = mid + 1; } else { hi_i = mid; }
+      }
+      for (uint32_t lo_i = w0, hi_i = wgs; lo_i < hi_i;) {  // last w with P[w] <= lo + slen - 1
+        const uint32_t mid = (lo_i + hi_i) >> 1;
+        if (P[mid] <= lo + slen - 1) { w1 = mid; lo_i = mid + 1; } else { hi_i = mid; }
+      }
+      for (uint32_t w = w0; w <= w1 && !late; ++w) {
+        const uint32_t want = min(kTreeWG, T->n - w * kTreeWG);
+        while (__hip_atomic_load(T->done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               want) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > T->wait_ticks) {
+            late = true;
+            break;
+          }
+        }
+      }
+    } else {
+      while (__hip_atomic_load(T->ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > T->wait_ticks) {
+          late = true;
+          break;
+        }
+      }
+    }
+    if (late) __hip_atomic_store(T->err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // the loads below stay after the wait (the flags were agent-scope loads)
+  __atomic_signal_fence(__ATOMIC_ACQUIRE);
+  uint32_t key[8], dek[8];
+  uint32_t base;
+  if (cid) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      key[i] = T->cid_key[i];
+      dek[i] = __builtin_amdgcn_readfirstlane(
+          load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i));
+    }
+    base = T->cid_base;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      key[i] = T->salt[i];
+      dek[i] = 0;
+    }
+    base = kKeyed;
+  }
+  const uint8_t *msg = T->lines + lo;
+  uint8_t *cmsg = T->ctext ? T->ctext + lo : nullptr;
+  uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (slen == kTreeSpan) {  // 64 full chunks: k_pass's staged lane layout (G = 1)
+    const uint32_t wl = lds_offset(lds_u4 + (threadIdx.x >> 6) * 512);
+    if (cid)
+      lane_subtree_full<1, true, true, A, kLoadCoherent>(
+          cv, msg, cmsg ? cmsg : const_cast<uint8_t *>(msg), l, false, key, base, dek, wl,
+          uint32_t(kTreeSpan), s * 64u, cmsg ? uint32_t(kTreeSpan) : 0u);
+    else
+      lane_subtree_full<1, false, true, A, kLoadCoherent>(cv, msg, nullptr, l, false, key, base,
+                                                          dek, wl, uint32_t(kTreeSpan), s * 64u);
+  } else if (l < C) {  // the blob's last span
+    const uint32_t clen = min(slen - l * 1024u, 1024u);
+    if (cid)
+      lane_chunk_coh<true>(cv, msg + l * 1024u, cmsg ? cmsg + l * 1024u : nullptr, clen,
+                           s * 64u + l, W == 1 && C == 1, key, base, dek);
+    else
+      lane_chunk_coh<false>(cv, msg + l * 1024u, nullptr, clen, s * 64u + l, W == 1 && C == 1,
+                            key, base, dek);
+  }
+  wave_merge<A>(cv, C, W == 1, key, base);
+  uint32_t last = W == 1;
+  if (W > 1) {  // the span's CV; the block's last span to finish merges them
+    uint32_t *scv = cid ? T->cid_cv : T->dek_cv;
+    if (l == 0) {
+      publish_cv(scv + uint64_t(g) * 8, cv);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the CV stores are done
+      last = __hip_atomic_fetch_add((cid ? T->cid_cnt : T->dek_cnt) + b, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == W;
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (last) {
+      if (l < W) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          cv[i] = load_cv_word(scv + (uint64_t(b) * spb + l) * 8 + i);
+      }
+      wave_merge<A>(cv, W, true, key, base);
+    }
+  }
+  if (last && l == 0) {
+    if (cid) {
+      store_digest(ref, cv);  // read by the next launch (the index node)
+    } else {
+      publish_cv(reinterpret_cast<uint32_t *>(ref + 32), cv);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(T->ready + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Blobs [b0, b0 + cnt) of the CID pass have their tree-line digits written:
+// count them into their entry group (the items never straddle a group).
+__device__ __forceinline__ void tree_done(const SArgs &a, uint64_t b0, uint32_t cnt) {
+  if (b0 >= a.n) return;  // (uniform)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's digit stores are done
+  if ((threadIdx.x & 63u) == 0) {
+    const uint32_t k = uint32_t(min<uint64_t>(cnt, a.n - b0));
+    __hip_atomic_fetch_add(a.tree->done + b0 / kTreeWG, k, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2157,11 +2420,23 @@ __global__ __launch_bounds__(256, GLFSX_SMALLQ_WPE) void k_small_q(SArgs a, uint
   const uint32_t waves = gridDim.x * 4u;
   const uint32_t lane = threadIdx.x & 63u;
   uint64_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
-  while (item < items) {  // wave-uniform
-    if (G == 1 || item < a.n_coarse)
+  // tree items (CID pass of the one-call tree route) come after the blobs'
+  // and only from the counter, never as a wave's first item: a tree item
+  // waits only for items handed out before it, to waves already running
+  const uint64_t tbase = items > waves ? items : uint64_t(waves);
+  const uint64_t end = (CHACHA && a.tree_items) ? tbase + a.tree_items : items;
+  while (item < end) {  // wave-uniform
+    if (item >= tbase) {
+      if constexpr (CHACHA) tree_item<A>(a, item - tbase, lds_u4);
+    } else if (item >= items) {
+      // a first item past the blobs: nothing
+    } else if (G == 1 || item < a.n_coarse) {
       small_blob<G, CHACHA, A>(a, (item << 6) | lane, lds_u4);
-    else if constexpr (G > 1)
+      if (CHACHA && a.tree) tree_done(a, item << 6, 64u);
+    } else if constexpr (G > 1) {
       small_fine<G, CHACHA, A>(a, fine0 + (item - a.n_coarse) * BPI, lds_u4);
+      if (CHACHA && a.tree) tree_done(a, fine0 + (item - a.n_coarse) * BPI, BPI);
+    }
     uint32_t t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2748,11 +3023,10 @@ hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
   hipError_t e = small_q_get(s, &ctr, &epoch);
   if (e != hipSuccess) return e;
   SArgs a = a0;
-  const uint32_t div = G > 1 ? kSmallFineDiv : 0u;
-  const uint64_t fine = div ? a.n / div : 0;
+  const uint64_t fine = G > 1 ? a.n / kSmallFineDiv : 0;
   a.n_coarse = (a.n - fine) >> 6;  // whole coarse items; the rest goes fine
   const uint64_t rest = a.n - (a.n_coarse << 6), bpi = G > 1 ? 64 / G : 64;
-  const uint64_t items = a.n_coarse + (rest + bpi - 1) / bpi;
+  const uint64_t items = a.n_coarse + (rest + bpi - 1) / bpi + (CHACHA ? a.tree_items : 0);
   const uint64_t wgs = (items + 3) / 4;
   const uint32_t grid = uint32_t(std::min<uint64_t>(wgs, slots ? slots : wgs));
   hipLaunchKernelGGL((k_small_q<G, CHACHA, A>), dim3(grid), dim3(256), 0, s, a, ctr, epoch);
@@ -2764,7 +3038,7 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
   const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
   const int gsel = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0;
-  if (grid.x <= latency_wgs()) {  // few blobs: the compiler's ARX form
+  if (grid.x <= latency_wgs() && !(CHACHA && a.tree_items)) {  // few blobs: the compiler's ARX form
     switch (gsel) {
       case 1: hipLaunchKernelGGL((k_small<1, CHACHA, false>), grid, block, 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_small<2, CHACHA, false>), grid, block, 0, s, a); break;
@@ -3037,6 +3311,8 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   a.out_off = 0;
   a.hex_out = job.hex_out;
   a.hex_pos = job.hex_pos;
+  a.tree = job.tree_items ? job.tree : nullptr;
+  a.tree_items = job.tree_items;
   if (job.cid_wait) {  // e.g. the tree lines' static parts, on another stream
     e = hipStreamWaitEvent(s, job.cid_wait, 0);
     if (e != hipSuccess) return e;

@@ -429,13 +429,20 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
 @pytest.mark.parametrize("n,tree_bs", [(70_000, 2 * MIB), (3000, 4096), (300, 64 * 1024),
                                        (1, 2 * MIB), (257, 1024),
                                        # one tree block at 8 MiB (its ref is
-                                       # the root); 5 blocks + an index node
-                                       (20_000, 8 * MIB), (20_000, MIB)])
+                                       # the root; no tree items: > 64 spans);
+                                       # 5 blocks + an index node
+                                       (20_000, 8 * MIB), (20_000, MIB),
+                                       # 64 spans per block (the most tree
+                                       # items take), 3 blocks; 2 spans per
+                                       # block, the last span partial
+                                       (40_000, 4 * MIB), (2_500, 128 * 1024)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
     """glfsx_post_tree_device (blob hashing, tree lines and the tree blob
-    overlapped) against the three calls in sequence on the same inputs:
-    ragged blob sizes 0..16 KiB at odd offsets, names with JSON escapes and
-    non-ASCII bytes, every blob root, every line byte, the tree root."""
+    overlapped: tree blocks of 64 KiB spans, at most 64 per block, are
+    hashed as work items of the blobs' CID pass) against the three calls in
+    sequence on the same inputs: ragged blob sizes 0..16 KiB at odd offsets,
+    names with JSON escapes and non-ASCII bytes, every blob root, every
+    line byte, the tree root."""
     import ctypes
     import random
     import torch
