@@ -285,6 +285,7 @@ struct OnePoster {
   int dev = -1;
   std::mutex mu;
   std::vector<OneReq *> pending;
+  std::atomic<size_t> npending{0};  // pending.size(), read without the lock
   std::atomic<bool> leader{false};
   OneLane lane[kOneLanes];
 };
@@ -397,6 +398,7 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
   {
     std::lock_guard<std::mutex> lk(P->mu);
     P->pending.insert(P->pending.end(), rs, rs + n);
+    P->npending.store(P->pending.size(), std::memory_order_release);
   }
   size_t ndone = 0;  // rs[0..ndone) are finished or failed
   for (uint32_t spins = 0;; ++spins) {
@@ -408,8 +410,12 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         if (rs[i]->rc) return fail(rs[i]->rc, "%s", rs[i]->err.c_str());
       return 0;
     }
+    // leadership only when there is something to launch and nobody holds it
+    // (many waiting callers must not bounce the word between cores)
     bool idle = false;
-    if (P->leader.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
+    if (P->npending.load(std::memory_order_acquire) &&
+        !P->leader.load(std::memory_order_relaxed) &&
+        P->leader.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
       // a lane whose last launch has completed
       OneLane *L = nullptr;
       int rc = 0;
@@ -441,6 +447,7 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         }
         batch.assign(P->pending.begin(), P->pending.begin() + k);
         P->pending.erase(P->pending.begin(), P->pending.begin() + k);
+        P->npending.store(P->pending.size(), std::memory_order_release);
       }
       if (!batch.empty()) {
         const uint32_t seq = ++L->seq;
