@@ -1946,10 +1946,14 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
   const uint32_t base = dp->cid_keyed ? kKeyed : 0u;
   uint32_t cl, ch;
   one_hash(cl, ch, img, ts, passbuf, slen, ckey, base, q, quad, rel, sidx << 6, false);
-  // this span's ctext stores are done before it counts in (the last
-  // workgroup signals the caller)
+  // this span's ctext is in the caller's staging before the span counts in
+  // (the last workgroup signals the caller): the stores are done, and a
+  // system-scope release writes back what this XCD's L2 holds of them --
+  // the staging may be non-coherent host memory, and the last workgroup's
+  // own release covers only its XCD
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0 && dp->flag) __threadfence_system();
   bool last;
   med_publish_merge(cl, ch, dp, sidx, W, ts, passbuf, &s_flag, ckey, base, q, quad, rel,
                     &last);
