@@ -3187,7 +3187,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     T.dek_cv = T.ready + blk_max;
     T.cid_cv = T.dek_cv + 8 * spans_max;
     T.err = reinterpret_cast<uint32_t *>(c->h_terr.dptr());
-    T.wait_ticks = 100000000ull;  // 1 s of s_memrealtime
+    fused_debug_take(&T.skip_block, &T.wait_ticks);  // (1 s of s_memrealtime unless a test set it)
     words_from_key(T.salt, tsalts.raw);
     memcpy(T.cid_key, sj.cid_key, 32);
     T.cid_base = sj.cid_keyed ? 16u : 0u;  // KEYED_HASH
@@ -3214,6 +3214,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   auto items_check = [&]() -> int {
     if (items && __atomic_load_n(reinterpret_cast<uint32_t *>(c->h_terr.p), __ATOMIC_ACQUIRE)) {
       tls_fused_failed = true;
+      fused_timeout_add();
       return fail(GLFSX_E_DEVICE, "a tree item's wait timed out; its results were discarded");
     }
     return 0;

@@ -49,6 +49,11 @@ uint32_t fused_errors_take(hipStream_t s);
 void fused_debug(uint32_t skip_msg, uint64_t wait_us);
 // Timeouts seen by fused_errors_take so far (process-wide).
 uint64_t fused_timeouts();
+// The same hooks for the one-call tree route's tree items: takes the pending
+// skip (a tree block whose DEK is computed but never flagged ready; ~0u:
+// none) and the wait bound; a timeout the host saw is counted.
+void fused_debug_take(uint32_t *skip, uint64_t *wait_ticks);
+void fused_timeout_add();
 // The bulk passes' clock probe on the current device (k_pass): out[0] =
 // shader-clock cycles, out[1] = 100 MHz ticks summed over every k_pass
 // workgroup since the last reset; reset: zero them after reading.
@@ -100,6 +105,7 @@ struct TreeItems {
   uint32_t salt[8];           // the tree's rawSalt (DEK key)
   uint32_t cid_key[8];
   uint32_t cid_base;          // kKeyed or 0
+  uint32_t skip_block;        // test hook: this block's DEK is never flagged (~0u: none)
 };
 constexpr uint64_t kTreeSpan = 64ull << 10;
 

@@ -2373,7 +2373,8 @@ __device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds
     } else {
       publish_cv(reinterpret_cast<uint32_t *>(ref + 32), cv);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(T->ready + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (b != T->skip_block)
+        __hip_atomic_store(T->ready + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -3146,6 +3147,13 @@ void fused_debug(uint32_t skip_msg, uint64_t wait_us) {
 }
 
 uint64_t fused_timeouts() { return g_dc_timeouts.load(std::memory_order_relaxed); }
+
+void fused_debug_take(uint32_t *skip, uint64_t *wait_ticks) {
+  *skip = g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed);
+  *wait_ticks = g_dc_wait_ticks.load(std::memory_order_relaxed);
+}
+
+void fused_timeout_add() { g_dc_timeouts.fetch_add(1, std::memory_order_relaxed); }
 
 void blake3_iv_words(uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) w[i] = kIV[i];
