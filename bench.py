@@ -1354,15 +1354,18 @@ def postblob_concurrency(N, ln=4096, plan=((1, 3000), (16, 1500), (64, 600), (25
     from glfs_amd import glfs
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libpostbench.so"))
     lib.postbench_run.restype = ctypes.c_int
-    lib.postbench_run.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p,
-                                  ctypes.c_int, ctypes.c_void_p]
+    lib.postbench_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_uint64,
+                                                           ctypes.c_int, ctypes.c_char_p,
+                                                           ctypes.c_int, ctypes.c_void_p]
+    fns = [ctypes.cast(getattr(N.lib, f), ctypes.c_void_p).value
+           for f in ("glfsx_create", "glfsx_set_device", "glfsx_sink_count")]
     salt = glfs.Machine().make_salt("blob")
     import torch
     dev = int(torch.cuda.current_device())
     res = {}
     for threads, calls in plan:
         out = (ctypes.c_double * 5)()
-        rc = lib.postbench_run(threads, ln, calls, salt, dev, out)
+        rc = lib.postbench_run(*fns, threads, ln, calls, salt, dev, out)
         N.check(rc, "postbench")
         res[str(threads)] = {"calls_per_s": round(out[0] / out[1]), "calls": int(out[0]),
                              "p50_us": round(out[2], 1), "p90_us": round(out[3], 1),

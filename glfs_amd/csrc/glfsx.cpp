@@ -167,16 +167,16 @@ int ctx_get(Ctx **out) {
 
 // Wait for a stream whose results the caller is about to return.  Polls
 // for up to kSpinNs first: a blocking hipStreamSynchronize wakes the thread
-// tens of microseconds after the GPU finishes, which is most of the host
-// overhead of a short call (a 1 GiB Create takes ~1.3 ms); longer waits block.
-// At most kMaxSpinners threads poll at once (glfs.Machine is used
-// concurrently; N pollers would pin N host cores); the rest block at once,
-// and a poller yields its core between queries.
-// GLFSX_SPIN_US overrides the poll bound (A/B: config 4's 4.9 ms call waited
-// its last ~3 ms blocked at the 2 ms default)
+// tens to hundreds of microseconds after the GPU finishes, which is most of
+// the host overhead of a short call (a 1 GiB Create takes ~1.3 ms, config
+// 4's one call ~5 ms: at a 2 ms bound it waited its last ~3 ms blocked and
+// lost ~0.1 ms to the wake-up); longer waits block.  At most kMaxSpinners
+// threads poll at once (glfs.Machine is used concurrently; N pollers would
+// pin N host cores); the rest block at once, and a poller yields its core
+// between queries.  GLFSX_SPIN_US overrides the poll bound (default 20 ms).
 const int64_t kSpinNs = [] {
   const char *e = getenv("GLFSX_SPIN_US");
-  return e ? int64_t(strtoll(e, nullptr, 10)) * 1000 : int64_t(2000000);
+  return e ? int64_t(strtoll(e, nullptr, 10)) * 1000 : int64_t(20000000);
 }();
 constexpr int kMaxSpinners = 4;
 std::atomic<int> g_spinners{0};
@@ -257,6 +257,7 @@ constexpr int kOneLanes = 8;
 struct OneLane;
 struct OneReq {
   OneDesc d{};
+  OneReq *next = nullptr;     // the pending stack
   std::atomic<int> armed{0};  // flag / seq / lane below are set (by the leader)
   std::atomic<int> done{0};   // failed before launch (rc, err)
   const uint32_t *flag = nullptr;
@@ -283,22 +284,21 @@ constexpr uint64_t kMedBatchBytes = 64ull << 20;  // device copies per launch
 constexpr size_t kMedAuxWords = 64 * 8 + 8 + 8;   // cvs, dek, cnt (+ pad)
 struct OnePoster {
   int dev = -1;
-  std::mutex mu;
-  std::vector<OneReq *> pending;
-  std::atomic<size_t> npending{0};  // pending.size(), read without the lock
+  // requests not yet launched: a lock-free stack (many callers push, the
+  // leader takes it whole)
+  std::atomic<OneReq *> pending{nullptr};
   std::atomic<bool> leader{false};
   OneLane lane[kOneLanes];
 };
-std::mutex g_posters_mu;
-std::vector<OnePoster *> g_posters;  // one per device, process lifetime
+constexpr int kMaxPosterDevs = 64;
+std::mutex g_posters_mu;                               // creation only
+std::atomic<OnePoster *> g_posters[kMaxPosterDevs];    // one per device, process lifetime
 
 int poster_get(int dev, OnePoster **out) {
+  if (dev < 0 || dev >= kMaxPosterDevs) return fail(GLFSX_E_DEVICE, "device %d", dev);
+  if ((*out = g_posters[dev].load(std::memory_order_acquire))) return 0;
   std::lock_guard<std::mutex> lk(g_posters_mu);
-  for (OnePoster *p : g_posters)
-    if (p->dev == dev) {
-      *out = p;
-      return 0;
-    }
+  if ((*out = g_posters[dev].load(std::memory_order_acquire))) return 0;
   auto *p = new OnePoster();
   p->dev = dev;
   for (OneLane &l : p->lane) {
@@ -326,9 +326,17 @@ int poster_get(int dev, OnePoster **out) {
     l.d_flag = static_cast<uint32_t *>(df);
     memset(hf, 0, sizeof(uint32_t) * kOneBatch);
   }
-  g_posters.push_back(p);
+  g_posters[dev].store(p, std::memory_order_release);
   *out = p;
   return 0;
+}
+
+void pending_push(OnePoster *P, OneReq *r) {
+  OneReq *h = P->pending.load(std::memory_order_relaxed);
+  do {
+    r->next = h;
+  } while (!P->pending.compare_exchange_weak(h, r, std::memory_order_release,
+                                             std::memory_order_relaxed));
 }
 
 // One launch of k_one over the batch's small messages and one launch_med
@@ -395,11 +403,7 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
       return fail(GLFSX_E_ARG, "one-shot post: bad descriptor");
   OnePoster *P;
   if (int e = poster_get(dev, &P)) return e;
-  {
-    std::lock_guard<std::mutex> lk(P->mu);
-    P->pending.insert(P->pending.end(), rs, rs + n);
-    P->npending.store(P->pending.size(), std::memory_order_release);
-  }
+  for (size_t i = 0; i < n; ++i) pending_push(P, rs[i]);
   size_t ndone = 0;  // rs[0..ndone) are finished or failed
   for (uint32_t spins = 0;; ++spins) {
     while (ndone < n && (rs[ndone]->done.load(std::memory_order_acquire) ||
@@ -413,7 +417,7 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
     // leadership only when there is something to launch and nobody holds it
     // (many waiting callers must not bounce the word between cores)
     bool idle = false;
-    if (P->npending.load(std::memory_order_acquire) &&
+    if (P->pending.load(std::memory_order_relaxed) &&
         !P->leader.load(std::memory_order_relaxed) &&
         P->leader.compare_exchange_strong(idle, true, std::memory_order_acq_rel)) {
       // a lane whose last launch has completed
@@ -432,22 +436,23 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
       }
       std::vector<OneReq *> batch;
       if (L) {
-        std::lock_guard<std::mutex> lk(P->mu);
         // up to kOneBatch requests, at most kMedBatchBytes of medium ones
-        // (always at least one request)
-        size_t k = 0;
+        // (always at least one request); the rest goes back on the stack
+        OneReq *r = P->pending.exchange(nullptr, std::memory_order_acquire);
         uint64_t mb = 0;
-        while (k < P->pending.size() && k < kOneBatch) {
-          const uint64_t len = P->pending[k]->d.len;
-          if (len > kMaxOneLen) {
-            if (k && mb + len > kMedBatchBytes) break;
-            mb += len;
+        while (r) {
+          OneReq *nx = r->next;
+          const uint64_t len = r->d.len;
+          const bool fits = batch.size() < kOneBatch &&
+                            (len <= kMaxOneLen || batch.empty() || mb + len <= kMedBatchBytes);
+          if (fits) {
+            if (len > kMaxOneLen) mb += len;
+            batch.push_back(r);
+          } else {
+            pending_push(P, r);
           }
-          ++k;
+          r = nx;
         }
-        batch.assign(P->pending.begin(), P->pending.begin() + k);
-        P->pending.erase(P->pending.begin(), P->pending.begin() + k);
-        P->npending.store(P->pending.size(), std::memory_order_release);
       }
       if (!batch.empty()) {
         const uint32_t seq = ++L->seq;
@@ -3120,20 +3125,21 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   } else {
     blake3_iv_words(sj.cid_key);
   }
-  // The tree blob's blocks as work items of the blobs' CID pass (TreeItems):
-  // tree blocks of whole 64 KiB spans, at most 64 per block, 16-B aligned
-  // buffers (else, or when repeating a failed call, the tree blob is posted
-  // after the CID pass).  Counters and flags are zeroed on B before the
-  // layout, sized for the line buffer's capacity.
+  // The tree blob as the work items of one persistent launch after the
+  // blobs' CID pass (TreeItems, k_tree_items): tree blocks of whole 64 KiB
+  // spans, at most 64 per block, 16-B aligned buffers (else, or when
+  // repeating a failed call, the general post of the tree blob).  Counters
+  // and flags are zeroed on B before the layout, sized for the line
+  // buffer's capacity.
   const bool items = tls_fused && tree_bs % kTreeSpan == 0 && tree_bs / kTreeSpan <= 64 &&
                      ((reinterpret_cast<uintptr_t>(d_lines) |
                        reinterpret_cast<uintptr_t>(d_tree_ctext)) & 15) == 0;
   const uint64_t spans_max = (lines_cap + kTreeSpan - 1) / kTreeSpan;
   const uint64_t blk_max = (lines_cap + tree_bs - 1) / tree_bs;
-  // words after the struct: done[wgs], dek_cnt / cid_cnt / ready[blk_max],
-  // then the CVs (2 x 8 words per span)
+  // after the struct: dek_cnt / cid_cnt / ready [blk_max], then 2 x 8 CV
+  // words per span
   const uint64_t ti_hdr = (sizeof(TreeItems) + 255) / 256 * 256;
-  const uint64_t ti_zero = 4 * (wgs + 3 * blk_max);
+  const uint64_t ti_zero = 4 * 3 * blk_max;
   if (items) {
     if (int e = c->d_titems.ensure(ti_hdr + ti_zero + 64 * spans_max + 64)) return e;
     if (int e = c->h_titems.ensure(sizeof(TreeItems))) return e;
@@ -3151,7 +3157,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   sj.hex_out = static_cast<uint8_t *>(d_lines);
   sj.hex_pos = tj.hex_pos;
   sj.cid_wait = ev_static;
-  if (!items) HIP_TRY(launch_post_small(sj, A));
+  HIP_TRY(launch_post_small(sj, A));
   // the layout (beside the DEK pass) gives the tree blob's size
   HIP_TRY(hipEventSynchronize(ev_layout));
   const uint64_t total = static_cast<const uint64_t *>(c->h_tree.p)[wgs];
@@ -3161,12 +3167,12 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     return fail(GLFSX_E_ARG, "tree lines need %llu bytes, buffer holds %llu",
                 (unsigned long long)total, (unsigned long long)lines_cap);
   }
+  // the tree blob, on A after the CID pass (its lines are complete then)
   const uint64_t nblk = (total + tree_bs - 1) / tree_bs;
   const uint64_t n1 = (nblk + tree_bs / 64 - 1) / (tree_bs / 64);
   if (int e = level_prepare(c->d_lvl_a, nblk, n1, tree_bs, A)) return e;
   uint8_t *lvl = c->d_lvl_a.u8();
   if (items) {
-    // the blobs' CID pass with the tree blob's items behind them
     TreeItems &T = *static_cast<TreeItems *>(c->h_titems.p);
     T = TreeItems{};
     uint32_t *z = reinterpret_cast<uint32_t *>(c->d_titems.u8() + ti_hdr);
@@ -3177,11 +3183,7 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     T.bs = tree_bs;
     T.spans = uint32_t((total + kTreeSpan - 1) / kTreeSpan);
     T.spb = uint32_t(tree_bs / kTreeSpan);
-    T.n = uint32_t(n);
-    T.wgs = uint32_t(wgs);
-    T.wg_prefix = tj.scratch + n;  // then the total (k_tree_prefix)
-    T.done = z;
-    T.dek_cnt = z + wgs;
+    T.dek_cnt = z;
     T.cid_cnt = T.dek_cnt + blk_max;
     T.ready = T.cid_cnt + blk_max;
     T.dek_cv = T.ready + blk_max;
@@ -3192,11 +3194,8 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     memcpy(T.cid_key, sj.cid_key, 32);
     T.cid_base = sj.cid_keyed ? 16u : 0u;  // KEYED_HASH
     HIP_TRY(hipMemcpyAsync(c->d_titems.p, &T, sizeof T, hipMemcpyHostToDevice, A));
-    sj.tree = reinterpret_cast<const TreeItems *>(c->d_titems.p);
-    sj.tree_items = 2ull * T.spans;
-    HIP_TRY(launch_post_small(sj, A));
+    HIP_TRY(launch_tree_items(reinterpret_cast<const TreeItems *>(c->d_titems.p), T.spans, A));
   } else {
-    // the tree blob, on A after the CID pass (its lines are complete then)
     PostJob j{};
     j.src = static_cast<const uint8_t *>(d_lines);
     j.ctext = static_cast<uint8_t *>(d_tree_ctext);

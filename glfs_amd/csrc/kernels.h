@@ -81,23 +81,20 @@ constexpr uint64_t kMaxSmallLen = 16ull * 1024;
 // entries per workgroup of the tree-line kernels (tree_kernels.hip)
 constexpr uint32_t kTreeWG = 256;
 // The tree blob of the one-call config-4 route (glfsx_post_tree_device) as
-// work items of the blobs' CID pass (k_small_q), after the blobs' items: the
-// blob is cut into 64 KiB spans (tree block size a multiple of 64 KiB); a
-// DEK item hashes one span (one chunk per lane) as soon as every entry whose
-// line touches it has its hex digits written (done[] per entry group of
-// kTreeWG), a CID item as soon as its block's DEK is published (ready[]);
-// the last span of a block to finish merges the block's span CVs.  Refs land
-// at refs + 64 b (the level-1 node image).  In device memory; counters zero
-// before the launch.
+// work items of one persistent launch after the blobs' CID pass has written
+// its lines (k_tree_items): the blob is cut into 64 KiB spans (tree block
+// size a multiple of 64 KiB, at most 64 spans per block); a DEK item hashes
+// one span (one chunk per lane), the last span of a block to finish merges
+// the block's span CVs into its DEK and flags it ready; a CID item waits for
+// its block's DEK, then the same with the keystream.  Refs land at refs +
+// 64 b (the level-1 node image).  In device memory; counters zero before
+// the launch.
 struct TreeItems {
   const uint8_t *lines;       // the tree blob, 16-B aligned
   uint8_t *ctext;             // nullable, 16-B aligned
   uint8_t *refs;              // 64 B per tree block
   uint64_t total, bs;         // blob bytes, tree block size
   uint32_t spans, spb;        // 64 KiB spans of the blob, per block
-  uint32_t n, wgs;            // entries, entry groups
-  const uint64_t *wg_prefix;  // exclusive line prefix per entry group, then the total
-  uint32_t *done;             // per entry group: entries with their digits written
   uint32_t *dek_cnt, *cid_cnt, *ready;  // per tree block
   uint32_t *dek_cv, *cid_cv;  // 8 words per span
   uint32_t *err;              // pinned host word: 3 when a wait timed out
@@ -128,16 +125,13 @@ struct SmallJob {
   const uint64_t *hex_pos;
   hipEvent_t cid_wait;  // nullable: the CID pass waits for it (after the DEK pass)
   uint32_t passes;      // 1: the DEK pass only, 2: the CID pass only, 0: both
-  // CID pass: the tree blob's items (device memory, see TreeItems) and their
-  // count (2 x spans; 0: none).  Needs the many-wave form (k_small_q):
-  // launch_post_small fails with hipErrorInvalidValue otherwise.
-  const TreeItems *tree;
-  uint64_t tree_items;
 };
 
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
+// The tree items of d_tree (device memory, 2 x spans items) in one launch.
+hipError_t launch_tree_items(const TreeItems *d_tree, uint32_t spans, hipStream_t s);
 
 // One-shot posts (ref.go:98-161 for one message of at most kMaxOneLen bytes:
 // a glfs.PostBlob of a small blob, a Writer's tail block, an index node of a

@@ -1986,10 +1986,6 @@ struct SArgs {
   uint64_t small_max;  // longer blobs are skipped (SmallJob::small_max)
   uint8_t *hex_out;    // CID pass, nullable: the root as tree-line hex digits
   const uint64_t *hex_pos;
-  // CID pass of the one-call tree route: the tree blob's work items after
-  // the blobs' (TreeItems, device memory; nullptr and 0 otherwise)
-  const TreeItems *tree;
-  uint64_t tree_items;
 };
 
 // Lower-case hex digits of bytes 0 and 1 of x, in output order (hi(b0)
@@ -2005,10 +2001,7 @@ __device__ __forceinline__ uint32_t hex4(uint32_t x) {
 // of a TreeEntry line, encoding as tree_kernels.hip's hex32) at dst, any
 // alignment: aligned 4-byte stores of the digits shifted into place
 // (alignbyte), the two partial words at the ends byte by byte -- no byte
-// outside [dst, dst + 64) is written.  COH: device-coherent (agent-scope
-// atomic) stores, for lines that tree items on other XCDs read in the same
-// launch.
-template <bool COH = false>
+// outside [dst, dst + 64) is written.
 __device__ __forceinline__ void put_hex32(uint8_t *dst, const uint32_t w[8]) {
   const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(dst) & 3u);
   const uint32_t sh = 8u * (4u - s);  // s = 0: the whole next word
@@ -2019,20 +2012,11 @@ __device__ __forceinline__ void put_hex32(uint8_t *dst, const uint32_t w[8]) {
     const uint32_t cur = k < 16 ? hex4(w[k >> 1] >> (16 * (k & 1))) : 0u;
     const uint32_t v = uint32_t(((uint64_t(cur) << 32) | prev) >> sh);
     if ((k >= 1 && k <= 15) || (k == 0 && s == 0)) {
-      if constexpr (COH)
-        __hip_atomic_store(base + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        base[k] = v;
+      base[k] = v;
     } else {
       const uint32_t lo = k == 0 ? s : 0u, hi = k == 0 ? 4u : s;
       uint8_t *b = reinterpret_cast<uint8_t *>(base + k);
-      for (uint32_t x = lo; x < hi; ++x) {
-        if constexpr (COH)
-          __hip_atomic_store(b + x, uint8_t(v >> (8u * x)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else
-          b[x] = uint8_t(v >> (8u * x));
-      }
+      for (uint32_t x = lo; x < hi; ++x) b[x] = uint8_t(v >> (8u * x));
     }
     prev = cur;
   }
@@ -2092,13 +2076,8 @@ __device__ __forceinline__ void small_blob(const SArgs &a, uint64_t i, uint4 *ld
   if (CHACHA && a.hex_out) {  // the tree line's cid and dek digits
     const uint64_t pos = a.hex_pos[i];
     if (pos != ~0ull) {  // ~0: the lines did not fit their buffer
-      if (a.tree) {
-        put_hex32<true>(a.hex_out + pos, cv);
-        put_hex32<true>(a.hex_out + pos + kDekAfterCid, dek);
-      } else {
-        put_hex32(a.hex_out + pos, cv);
-        put_hex32(a.hex_out + pos + kDekAfterCid, dek);
-      }
+      put_hex32(a.hex_out + pos, cv);
+      put_hex32(a.hex_out + pos + kDekAfterCid, dek);
     }
   }
 }
@@ -2164,13 +2143,8 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
     if (CHACHA && a.hex_out) {
       const uint64_t pos = a.hex_pos[i];
       if (pos != ~0ull) {
-        if (a.tree) {
-          put_hex32<true>(a.hex_out + pos, cv);
-          put_hex32<true>(a.hex_out + pos + kDekAfterCid, dek);
-        } else {
-          put_hex32(a.hex_out + pos, cv);
-          put_hex32(a.hex_out + pos + kDekAfterCid, dek);
-        }
+        put_hex32(a.hex_out + pos, cv);
+        put_hex32(a.hex_out + pos + kDekAfterCid, dek);
       }
     }
   }
@@ -2202,59 +2176,13 @@ __device__ __forceinline__ void wave_merge(uint32_t (&cv)[8], uint32_t cnt, bool
   }
 }
 
-// Device-coherent loads of bytes other XCDs wrote during the launch (the
-// tree lines' hex digits: put_hex32<true>): agent-scope atomic loads,
-// which do not return a stale line of this XCD's L2.
-__device__ __forceinline__ uint32_t coh_word(const uint8_t *p, uint32_t avail) {
-  if (avail >= 4)
-    return __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t w = 0;
-  for (uint32_t b = 0; b < avail; ++b)
-    w |= uint32_t(__hip_atomic_load(p + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-         << (8 * b);
-  return w;
-}
-
-// One chunk of clen (<= 1024) bytes at p (4-B aligned), chunk counter
-// `chunk`, through device-coherent loads: the tree items' partial span (the
-// blob's last).  CHACHA: the keystream of dek XORed in first, the ctext
-// stored at cp (nullable).  root: the chunk is the whole message.
-template <bool CHACHA>
-__device__ void lane_chunk_coh(uint32_t (&cv)[8], const uint8_t *p, uint8_t *cp, uint32_t clen,
-                               uint32_t chunk, bool root, const uint32_t (&key)[8],
-                               uint32_t base, const uint32_t (&dek)[8]) {
-  const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) cv[i] = key[i];
-  for (uint32_t b = 0; b < nb; ++b) {
-    const uint32_t avail = clen - min(clen, 64u * b) < 64u ? clen - min(clen, 64u * b) : 64u;
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      m[i] = uint32_t(4 * i) < avail ? coh_word(p + 64 * b + 4 * i, avail - 4 * i) : 0u;
-    if constexpr (CHACHA) {
-      uint32_t x[16];
-      chacha_block<0>(x, dek, (chunk << 4) + b);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] ^= x[i];
-      if (avail < 64) mask_tail(m, avail);
-      if (cp) store_block<false>(cp + 64 * b, m, avail);
-    }
-    uint32_t fl = base;
-    if (b == 0) fl |= kChunkStart;
-    if (b + 1 == nb) fl |= kChunkEnd | (root ? kRoot : 0u);
-    b3_compress<0>(cv, m, chunk, 0u, avail, fl);
-  }
-}
-
-// Tree item t (of 2 x spans): t < spans = the DEK item of span t, else the
-// CID item of span t - spans.  The whole wave runs it; lane l hashes chunk
-// l of the span.  Waits are bounded by T->wait_ticks (a timeout sets *err;
-// the host then discards the call's results).
+// Tree item t (of 2 x spans) of k_tree_items: t < spans = the DEK item of
+// span t, else the CID item of span t - spans.  The whole wave runs it; lane
+// l hashes chunk l of the span.  A CID item waits (bounded by T->wait_ticks;
+// a timeout sets *err and the host discards the call's results) for its
+// block's DEK.
 template <int A>
-__device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds_u4) {
-  const TreeItems *T = a.tree;
+__device__ __forceinline__ void tree_item(const TreeItems *T, uint64_t t, uint4 *lds_u4) {
   const uint32_t spans = T->spans, spb = T->spb;
   const bool cid = t >= spans;
   const uint32_t g = uint32_t(cid ? t - spans : t);
@@ -2267,50 +2195,21 @@ __device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds
   const uint32_t C = (slen + 1023) >> 10;                          // chunks of span g
   const uint32_t l = threadIdx.x & 63u;
   uint8_t *ref = T->refs + 64ull * b;
-  if (l == 0) {  // the wait: the span's entries (DEK) or the block's DEK (CID)
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool late = false;
-    if (!cid) {
-      // entry groups whose lines touch [lo, lo + slen): w0 = the group that
-      // holds byte lo, w1 = the one that holds byte lo + slen - 1
-      const uint64_t *P = T->wg_prefix;
-      const uint32_t wgs = T->wgs;
-      uint32_t w0 = 0, w1 = 0;
-      for (uint32_t lo_i = 0, hi_i = wgs; lo_i < hi_i;) {  // last w with P[w] <= lo
-        const uint32_t mid = (lo_i + hi_i) >> 1;
-        if (P[mid] <= lo) { w0 = mid; lo_i = mid + 1; } else { hi_i = mid; }
-      }
-      for (uint32_t lo_i = w0, hi_i = wgs; lo_i < hi_i;) {  // last w with P[w] <= lo + slen - 1
-        const uint32_t mid = (lo_i + hi_i) >> 1;
-        if (P[mid] <= lo + slen - 1) { w1 = mid; lo_i = mid + 1; } else { hi_i = mid; }
-      }
-      for (uint32_t w = w0; w <= w1 && !late; ++w) {
-        const uint32_t want = min(kTreeWG, T->n - w * kTreeWG);
-        while (__hip_atomic_load(T->done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-               want) {
-          __builtin_amdgcn_s_sleep(2);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > T->wait_ticks) {
-            late = true;
-            break;
-          }
-        }
-      }
-    } else {
+  uint32_t key[8], dek[8];
+  uint32_t base;
+  if (cid) {
+    if (l == 0) {  // the block's DEK (published with its ready flag)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(T->ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         __builtin_amdgcn_s_sleep(2);
         if (__builtin_amdgcn_s_memrealtime() - t0 > T->wait_ticks) {
-          late = true;
+          __hip_atomic_store(T->err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
     }
-    if (late) __hip_atomic_store(T->err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // the loads below stay after the wait (the flags were agent-scope loads)
-  __atomic_signal_fence(__ATOMIC_ACQUIRE);
-  uint32_t key[8], dek[8];
-  uint32_t base;
-  if (cid) {
+    // the loads below stay after the wait (the flag was an agent-scope load)
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       key[i] = T->cid_key[i];
@@ -2331,21 +2230,20 @@ __device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds
   uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (slen == kTreeSpan) {  // 64 full chunks: k_pass's staged lane layout (G = 1)
     const uint32_t wl = lds_offset(lds_u4 + (threadIdx.x >> 6) * 512);
-    if (cid)
-      lane_subtree_full<1, true, true, A, kLoadCoherent>(
-          cv, msg, cmsg ? cmsg : const_cast<uint8_t *>(msg), l, false, key, base, dek, wl,
-          uint32_t(kTreeSpan), s * 64u, cmsg ? uint32_t(kTreeSpan) : 0u);
+    if (cid)  // (no ctext wanted: the staged stores fall outside a 0-byte descriptor)
+      lane_subtree_full<1, true, true, A>(cv, msg, cmsg ? cmsg : const_cast<uint8_t *>(msg), l,
+                                          false, key, base, dek, wl, uint32_t(kTreeSpan),
+                                          s * 64u, cmsg ? uint32_t(kTreeSpan) : 0u);
     else
-      lane_subtree_full<1, false, true, A, kLoadCoherent>(cv, msg, nullptr, l, false, key, base,
-                                                          dek, wl, uint32_t(kTreeSpan), s * 64u);
-  } else if (l < C) {  // the blob's last span
-    const uint32_t clen = min(slen - l * 1024u, 1024u);
+      lane_subtree_full<1, false, true, A>(cv, msg, nullptr, l, false, key, base, dek, wl,
+                                           uint32_t(kTreeSpan), s * 64u);
+  } else if (l < C) {  // the blob's last span: chunk l of slen bytes
+    const bool one = W == 1 && C == 1;  // the chunk is the whole block
     if (cid)
-      lane_chunk_coh<true>(cv, msg + l * 1024u, cmsg ? cmsg + l * 1024u : nullptr, clen,
-                           s * 64u + l, W == 1 && C == 1, key, base, dek);
+      lane_subtree<1, true, true, A>(cv, msg, cmsg, slen, l, 1, one, key, base, dek, s * 64u);
     else
-      lane_chunk_coh<false>(cv, msg + l * 1024u, nullptr, clen, s * 64u + l, W == 1 && C == 1,
-                            key, base, dek);
+      lane_subtree<1, false, true, A>(cv, msg, nullptr, slen, l, 1, one, key, base, dek,
+                                      s * 64u);
   }
   wave_merge<A>(cv, C, W == 1, key, base);
   uint32_t last = W == 1;
@@ -2379,15 +2277,33 @@ __device__ __forceinline__ void tree_item(const SArgs &a, uint64_t t, uint4 *lds
   }
 }
 
-// Blobs [b0, b0 + cnt) of the CID pass have their tree-line digits written:
-// count them into their entry group (the items never straddle a group).
-__device__ __forceinline__ void tree_done(const SArgs &a, uint64_t b0, uint32_t cnt) {
-  if (b0 >= a.n) return;  // (uniform)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's digit stores are done
-  if ((threadIdx.x & 63u) == 0) {
-    const uint32_t k = uint32_t(min<uint64_t>(cnt, a.n - b0));
-    __hip_atomic_fetch_add(a.tree->done + b0 / kTreeWG, k, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+// The tree blob of the one-call config-4 route (TreeItems) after the blobs'
+// CID pass has written its lines: DEK items of the 64 KiB spans (one chunk
+// per lane), then their CID items, as many waves as the chip holds taking
+// items from a counter (bank epoch & 1 of two, the other zeroed by workgroup
+// 0 for the next launch on the stream).  A CID item only ever comes from the
+// counter, after every DEK item has been handed out to a running wave.
+template <int A>
+__global__ __launch_bounds__(256, 4) void k_tree_items(const TreeItems *T, uint32_t *ctr,
+                                                       uint32_t epoch) {
+  __shared__ uint4 lds_u4[4 * 512];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(ctr + ((epoch + 1u) & 1u) * 32u, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t *mine = ctr + (epoch & 1u) * 32u;
+  const uint32_t S = T->spans;
+  const uint32_t waves = gridDim.x * 4u;
+  const uint32_t tb = S > waves ? S : waves;  // CID items start here
+  uint32_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
+  while (item < tb + S) {  // wave-uniform
+    if (item < S)
+      tree_item<A>(T, item, lds_u4);
+    else if (item >= tb)
+      tree_item<A>(T, uint64_t(S) + (item - tb), lds_u4);
+    uint32_t t = 0;
+    if ((threadIdx.x & 63u) == 0)
+      t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    item = waves + uint32_t(__builtin_amdgcn_readfirstlane(t));
   }
 }
 
@@ -2425,23 +2341,11 @@ __global__ __launch_bounds__(256, GLFSX_SMALLQ_WPE) void k_small_q(SArgs a, uint
   const uint32_t waves = gridDim.x * 4u;
   const uint32_t lane = threadIdx.x & 63u;
   uint64_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
-  // tree items (CID pass of the one-call tree route) come after the blobs'
-  // and only from the counter, never as a wave's first item: a tree item
-  // waits only for items handed out before it, to waves already running
-  const uint64_t tbase = items > waves ? items : uint64_t(waves);
-  const uint64_t end = (CHACHA && a.tree_items) ? tbase + a.tree_items : items;
-  while (item < end) {  // wave-uniform
-    if (item >= tbase) {
-      if constexpr (CHACHA) tree_item<A>(a, item - tbase, lds_u4);
-    } else if (item >= items) {
-      // a first item past the blobs: nothing
-    } else if (G == 1 || item < a.n_coarse) {
+  while (item < items) {  // wave-uniform
+    if (G == 1 || item < a.n_coarse)
       small_blob<G, CHACHA, A>(a, (item << 6) | lane, lds_u4);
-      if (CHACHA && a.tree) tree_done(a, item << 6, 64u);
-    } else if constexpr (G > 1) {
+    else if constexpr (G > 1)
       small_fine<G, CHACHA, A>(a, fine0 + (item - a.n_coarse) * BPI, lds_u4);
-      if (CHACHA && a.tree) tree_done(a, fine0 + (item - a.n_coarse) * BPI, BPI);
-    }
     uint32_t t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3031,7 +2935,7 @@ hipError_t launch_small_q(const SArgs &a0, hipStream_t s) {
   const uint64_t fine = G > 1 ? a.n / kSmallFineDiv : 0;
   a.n_coarse = (a.n - fine) >> 6;  // whole coarse items; the rest goes fine
   const uint64_t rest = a.n - (a.n_coarse << 6), bpi = G > 1 ? 64 / G : 64;
-  const uint64_t items = a.n_coarse + (rest + bpi - 1) / bpi + (CHACHA ? a.tree_items : 0);
+  const uint64_t items = a.n_coarse + (rest + bpi - 1) / bpi;
   const uint64_t wgs = (items + 3) / 4;
   const uint32_t grid = uint32_t(std::min<uint64_t>(wgs, slots ? slots : wgs));
   hipLaunchKernelGGL((k_small_q<G, CHACHA, A>), dim3(grid), dim3(256), 0, s, a, ctr, epoch);
@@ -3043,7 +2947,7 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   const uint64_t C = max_len ? (max_len + 1023) >> 10 : 1;
   const dim3 grid(uint32_t((a.n + 255) / 256)), block(256);
   const int gsel = C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : 0;
-  if (grid.x <= latency_wgs() && !(CHACHA && a.tree_items)) {  // few blobs: the compiler's ARX form
+  if (grid.x <= latency_wgs()) {  // few blobs: the compiler's ARX form
     switch (gsel) {
       case 1: hipLaunchKernelGGL((k_small<1, CHACHA, false>), grid, block, 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_small<2, CHACHA, false>), grid, block, 0, s, a); break;
@@ -3323,8 +3227,6 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   a.out_off = 0;
   a.hex_out = job.hex_out;
   a.hex_pos = job.hex_pos;
-  a.tree = job.tree_items ? job.tree : nullptr;
-  a.tree_items = job.tree_items;
   if (job.cid_wait) {  // e.g. the tree lines' static parts, on another stream
     e = hipStreamWaitEvent(s, job.cid_wait, 0);
     if (e != hipSuccess) return e;
@@ -3343,6 +3245,20 @@ hipError_t clock_probe(int reset, uint64_t out[2]) {
   if (!reset) return hipSuccess;
   const unsigned long long z[2] = {0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof z, 0, hipMemcpyHostToDevice);
+}
+
+hipError_t launch_tree_items(const TreeItems *d_tree, uint32_t spans, hipStream_t s) {
+  if (spans == 0) return hipSuccess;
+  static const uint32_t slots = resident_wgs(k_tree_items<GLFSX_SMALL_CID>);
+  uint32_t *ctr;
+  uint32_t epoch;
+  hipError_t e = small_q_get(s, &ctr, &epoch);
+  if (e != hipSuccess) return e;
+  const uint32_t wgs = (2 * spans + 3) / 4;
+  const uint32_t grid = std::min(wgs, slots ? slots : wgs);
+  hipLaunchKernelGGL(k_tree_items<GLFSX_SMALL_CID>, dim3(grid), dim3(256), 0, s, d_tree, ctr,
+                     epoch);
+  return hipGetLastError();
 }
 
 #if GLFSX_WGTIME

@@ -2,7 +2,8 @@
 config 4's small-blob kernels (bench.small_blobs) and the read side
 (batched getF decrypt over a --gib GiB blob at 1 MiB blocks), and config 4
 end to end (bench.config4_end_to_end: blobs, tree lines, tree blob).
-usage: python scripts/legs.py [small|read|both|config4|config4one] [--gib G]"""
+usage: python scripts/legs.py [small|read|both|config4|config4one|config4all|postblob|config2]
+       [--gib G]"""
 import ctypes
 import json
 import os
@@ -41,6 +42,13 @@ def main():
     if what == "config4one":   # the one-call route alone, 20 reps
         out["config4_one_call"] = bench.config4_end_to_end(torch, N, stream, sp, reps=20,
                                                            routes=("one_call",))
+    if what == "config4all":   # all three routes, as the bench line
+        out["config4_end_to_end"] = bench.config4_end_to_end(torch, N, stream, sp)
+    if what == "postblob":     # per-call latency and concurrent callers
+        out["postblob_latency"] = bench.postblob_latency(N)
+        out["postblob_concurrency"] = bench.postblob_concurrency(N)
+    if what == "config2":
+        out["config2"] = bench.config2_leg(torch, N, stream, sp)
     print(json.dumps(out), flush=True)
 
 

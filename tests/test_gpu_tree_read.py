@@ -437,9 +437,9 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
                                        # block, the last span partial
                                        (40_000, 4 * MIB), (2_500, 128 * 1024)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
-    """glfsx_post_tree_device (blob hashing, tree lines and the tree blob
-    overlapped: tree blocks of 64 KiB spans, at most 64 per block, are
-    hashed as work items of the blobs' CID pass) against the three calls in
+    """glfsx_post_tree_device (blob hashing and tree lines overlapped; tree
+    blocks of 64 KiB spans, at most 64 per block, hashed as the work items
+    of one launch, others by the general post) against the three calls in
     sequence on the same inputs: ragged blob sizes 0..16 KiB at odd offsets,
     names with JSON escapes and non-ASCII bytes, every blob root, every
     line byte, the tree root."""
@@ -590,9 +590,9 @@ def test_post_tree_device_keyed_cid_and_ctext(gpu, O):
 def test_post_tree_device_tree_item_timeout_repeats(gpu, O):
     """A tree item that gives up waiting must not fail silently: block 1's
     DEK is withheld from its CID items (glfsx_debug_fused), they time out
-    after 2 ms, and the call is repeated with the tree blob posted after the
-    blobs' CID pass -- same roots, lines and tree root as the three calls,
-    one failure counted; the next call (no fault) is clean."""
+    after 2 ms, and the call is repeated with the general post of the tree
+    blob -- same roots, lines and tree root as the three calls, one failure
+    counted; the next call (no fault) is clean."""
     import ctypes
     import torch
     from glfs_amd import _native as N

@@ -4,6 +4,8 @@
  * one Writer per blob, bs 2 MiB, the blob type salt, a counting sink that
  * receives every Post).  Measurement harness only -- not part of the
  * library; built by __graft_entry__.build() into tools/libpostbench.so.
+ * The library's entry points come in as function pointers (the caller's
+ * handle on libglfsx.so, or on a build variant for an A/B in one process).
  *
  * postbench_run: out[0] = calls completed, out[1] = wall seconds from the
  * first call to the last return (all threads released together), out[2] /
@@ -16,6 +18,13 @@
 #include <time.h>
 
 #include "../include/glfsx.h"
+
+typedef int (*create_fn)(uint64_t, uint64_t, const uint8_t *, const uint8_t *, const void *,
+                         uint64_t, glfsx_post_fn, void *, glfsx_root *);
+typedef int (*set_device_fn)(int);
+static create_fn create_p;
+static set_device_fn set_device_p;
+static glfsx_post_fn sink_p;
 
 static double now(void) {
   struct timespec t;
@@ -38,16 +47,14 @@ static void *worker(void *arg) {
   for (uint64_t i = 0; i < j->len + 8; i++) data[i] = (uint8_t)(i * 131 + 7 * j->id);
   uint64_t counts[2] = {0, 0};
   glfsx_root root;
-  if (glfsx_set_device(j->dev)) j->rc = -1;
+  if (set_device_p(j->dev)) j->rc = -1;
   for (int i = 0; i < 3 && !j->rc; i++)  /* warm the thread's context */
-    j->rc = glfsx_create(2u << 20, 2u << 20, j->salt, NULL, data, j->len, glfsx_sink_count,
-                         counts, &root);
+    j->rc = create_p(2u << 20, 2u << 20, j->salt, NULL, data, j->len, sink_p, counts, &root);
   pthread_barrier_wait(j->go);
   for (int i = 0; i < j->calls && !j->rc; i++) {
     if (j->len >= 8) memcpy(data, &i, sizeof i); /* a distinct blob per call */
     const double t = now();
-    j->rc = glfsx_create(2u << 20, 2u << 20, j->salt, NULL, data, j->len, glfsx_sink_count,
-                         counts, &root);
+    j->rc = create_p(2u << 20, 2u << 20, j->salt, NULL, data, j->len, sink_p, counts, &root);
     j->lat[i] = now() - t;
   }
   j->t_end = now();
@@ -60,9 +67,12 @@ static int cmp(const void *a, const void *b) {
   return x < y ? -1 : x > y;
 }
 
-int postbench_run(int threads, uint64_t len, int calls, const uint8_t *salt, int dev,
-                  double out[5]) {
-  if (threads < 1 || calls < 1) return -1;
+int postbench_run(void *create, void *set_device, void *sink, int threads, uint64_t len,
+                  int calls, const uint8_t *salt, int dev, double out[5]) {
+  if (threads < 1 || calls < 1 || !create || !set_device || !sink) return -1;
+  create_p = (create_fn)create;
+  set_device_p = (set_device_fn)set_device;
+  sink_p = (glfsx_post_fn)sink;
   pthread_t *th = (pthread_t *)calloc(threads, sizeof *th);
   job *jobs = (job *)calloc(threads, sizeof *jobs);
   double *lat = (double *)calloc((size_t)threads * calls, sizeof *lat);
