@@ -118,10 +118,6 @@ struct Ctx {
   hipStream_t stream2 = nullptr;
   std::vector<hipEvent_t> events;
   PinBuf h_tree;
-  // its tree items (TreeItems: the struct, then its counters and CVs) and
-  // their timeout word
-  DevBuf d_titems;
-  PinBuf h_titems, h_terr;
   ~Ctx() {
     // Process teardown may already have unloaded the HIP runtime; leak.
   }
@@ -3125,28 +3121,6 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   } else {
     blake3_iv_words(sj.cid_key);
   }
-  // The tree blob as the work items of one persistent launch after the
-  // blobs' CID pass (TreeItems, k_tree_items): tree blocks of whole 64 KiB
-  // spans, at most 64 per block, 16-B aligned buffers (else, or when
-  // repeating a failed call, the general post of the tree blob).  Counters
-  // and flags are zeroed on B before the layout, sized for the line
-  // buffer's capacity.
-  const bool items = tls_fused && tree_bs % kTreeSpan == 0 && tree_bs / kTreeSpan <= 64 &&
-                     ((reinterpret_cast<uintptr_t>(d_lines) |
-                       reinterpret_cast<uintptr_t>(d_tree_ctext)) & 15) == 0;
-  const uint64_t spans_max = (lines_cap + kTreeSpan - 1) / kTreeSpan;
-  const uint64_t blk_max = (lines_cap + tree_bs - 1) / tree_bs;
-  // after the struct: dek_cnt / cid_cnt / ready [blk_max], then 2 x 8 CV
-  // words per span
-  const uint64_t ti_hdr = (sizeof(TreeItems) + 255) / 256 * 256;
-  const uint64_t ti_zero = 4 * 3 * blk_max;
-  if (items) {
-    if (int e = c->d_titems.ensure(ti_hdr + ti_zero + 64 * spans_max + 64)) return e;
-    if (int e = c->h_titems.ensure(sizeof(TreeItems))) return e;
-    if (int e = c->h_terr.ensure(64)) return e;
-    __atomic_store_n(reinterpret_cast<uint32_t *>(c->h_terr.p), 0u, __ATOMIC_RELAXED);
-    HIP_TRY(hipMemsetAsync(c->d_titems.u8() + ti_hdr, 0, ti_zero, B));
-  }
   sj.passes = 1;  // the DEK pass: the critical path, queued first
   HIP_TRY(launch_post_small(sj, A));
   HIP_TRY(launch_tree_layout(tj, B));
@@ -3172,52 +3146,17 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
   const uint64_t n1 = (nblk + tree_bs / 64 - 1) / (tree_bs / 64);
   if (int e = level_prepare(c->d_lvl_a, nblk, n1, tree_bs, A)) return e;
   uint8_t *lvl = c->d_lvl_a.u8();
-  if (items) {
-    TreeItems &T = *static_cast<TreeItems *>(c->h_titems.p);
-    T = TreeItems{};
-    uint32_t *z = reinterpret_cast<uint32_t *>(c->d_titems.u8() + ti_hdr);
-    T.lines = static_cast<const uint8_t *>(d_lines);
-    T.ctext = static_cast<uint8_t *>(d_tree_ctext);
-    T.refs = lvl;
-    T.total = total;
-    T.bs = tree_bs;
-    T.spans = uint32_t((total + kTreeSpan - 1) / kTreeSpan);
-    T.spb = uint32_t(tree_bs / kTreeSpan);
-    T.dek_cnt = z;
-    T.cid_cnt = T.dek_cnt + blk_max;
-    T.ready = T.cid_cnt + blk_max;
-    T.dek_cv = T.ready + blk_max;
-    T.cid_cv = T.dek_cv + 8 * spans_max;
-    T.err = reinterpret_cast<uint32_t *>(c->h_terr.dptr());
-    fused_debug_take(&T.skip_block, &T.wait_ticks);  // (1 s of s_memrealtime unless a test set it)
-    words_from_key(T.salt, tsalts.raw);
-    memcpy(T.cid_key, sj.cid_key, 32);
-    T.cid_base = sj.cid_keyed ? 16u : 0u;  // KEYED_HASH
-    HIP_TRY(hipMemcpyAsync(c->d_titems.p, &T, sizeof T, hipMemcpyHostToDevice, A));
-    HIP_TRY(launch_tree_items(reinterpret_cast<const TreeItems *>(c->d_titems.p), T.spans, A));
-  } else {
-    PostJob j{};
-    j.src = static_cast<const uint8_t *>(d_lines);
-    j.ctext = static_cast<uint8_t *>(d_tree_ctext);
-    j.stride = tree_bs;
-    j.msg_len = tree_bs;
-    j.n = nblk;
-    j.last_len = total - (nblk - 1) * tree_bs;
-    j.out = RefLayout{lvl, ~0ull, 0};  // ref t at byte 64t
-    words_from_key(j.salt, tsalts.raw);
-    cid_words(j, cid_key);
-    HIP_TRY(launch_post(j, A, tls_fused));
-  }
-  // a tree item that gave up waiting invalidates the call: repeated with
-  // the tree blob posted after the CID pass (with_fused_retry)
-  auto items_check = [&]() -> int {
-    if (items && __atomic_load_n(reinterpret_cast<uint32_t *>(c->h_terr.p), __ATOMIC_ACQUIRE)) {
-      tls_fused_failed = true;
-      fused_timeout_add();
-      return fail(GLFSX_E_DEVICE, "a tree item's wait timed out; its results were discarded");
-    }
-    return 0;
-  };
+  PostJob j{};
+  j.src = static_cast<const uint8_t *>(d_lines);
+  j.ctext = static_cast<uint8_t *>(d_tree_ctext);
+  j.stride = tree_bs;
+  j.msg_len = tree_bs;
+  j.n = nblk;
+  j.last_len = total - (nblk - 1) * tree_bs;
+  j.out = RefLayout{lvl, ~0ull, 0};  // ref t at byte 64t
+  words_from_key(j.salt, tsalts.raw);
+  cid_words(j, cid_key);
+  HIP_TRY(launch_post(j, A, tls_fused));
   *lines_len = total;
   tree_root->size = total;
   tree_root->block_size = tree_bs;
@@ -3226,15 +3165,11 @@ int post_tree_device_impl(uint64_t n, uint64_t blob_bs, const uint8_t *blob_salt
     HIP_TRY(hipMemcpyAsync(c->h_root.p, lvl, 64, hipMemcpyDeviceToHost, A));
     HIP_TRY(stream_wait(A));  // (B is drained: A waited for its static lines)
     if (int e = fused_check(A)) return e;
-    if (int e = items_check()) return e;
     memcpy(tree_root->ref, c->h_root.p, 64);
     return 0;
   }
   uint64_t posts = 0;
-  if (int e = build_up(c, A, tsalts, cid_key, tree_bs, lvl, n1, &c->d_lvl_b, tree_root->ref,
-                       &posts))
-    return e;
-  return items_check();
+  return build_up(c, A, tsalts, cid_key, tree_bs, lvl, n1, &c->d_lvl_b, tree_root->ref, &posts);
 }
 }  // namespace
 

@@ -52,8 +52,6 @@ uint64_t fused_timeouts();
 // The same hooks for the one-call tree route's tree items: takes the pending
 // skip (a tree block whose DEK is computed but never flagged ready; ~0u:
 // none) and the wait bound; a timeout the host saw is counted.
-void fused_debug_take(uint32_t *skip, uint64_t *wait_ticks);
-void fused_timeout_add();
 // The bulk passes' clock probe on the current device (k_pass): out[0] =
 // shader-clock cycles, out[1] = 100 MHz ticks summed over every k_pass
 // workgroup since the last reset; reset: zero them after reading.
@@ -80,32 +78,6 @@ hipError_t launch_chacha_xor(const uint32_t k[8], const uint8_t *src,
 constexpr uint64_t kMaxSmallLen = 16ull * 1024;
 // entries per workgroup of the tree-line kernels (tree_kernels.hip)
 constexpr uint32_t kTreeWG = 256;
-// The tree blob of the one-call config-4 route (glfsx_post_tree_device) as
-// work items of one persistent launch after the blobs' CID pass has written
-// its lines (k_tree_items): the blob is cut into 64 KiB spans (tree block
-// size a multiple of 64 KiB, at most 64 spans per block); a DEK item hashes
-// one span (one chunk per lane), the last span of a block to finish merges
-// the block's span CVs into its DEK and flags it ready; a CID item waits for
-// its block's DEK, then the same with the keystream.  Refs land at refs +
-// 64 b (the level-1 node image).  In device memory; counters zero before
-// the launch.
-struct TreeItems {
-  const uint8_t *lines;       // the tree blob, 16-B aligned
-  uint8_t *ctext;             // nullable, 16-B aligned
-  uint8_t *refs;              // 64 B per tree block
-  uint64_t total, bs;         // blob bytes, tree block size
-  uint32_t spans, spb;        // 64 KiB spans of the blob, per block
-  uint32_t *dek_cnt, *cid_cnt, *ready;  // per tree block
-  uint32_t *dek_cv, *cid_cv;  // 8 words per span
-  uint32_t *err;              // pinned host word: 3 when a wait timed out
-  uint64_t wait_ticks;        // the waits' bound (100 MHz ticks)
-  uint32_t salt[8];           // the tree's rawSalt (DEK key)
-  uint32_t cid_key[8];
-  uint32_t cid_base;          // kKeyed or 0
-  uint32_t skip_block;        // test hook: this block's DEK is never flagged (~0u: none)
-};
-constexpr uint64_t kTreeSpan = 64ull << 10;
-
 struct SmallJob {
   const uint8_t *src;
   uint8_t *ctext;  // nullable; same offsets as src
@@ -131,7 +103,6 @@ struct SmallJob {
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
 // The tree items of d_tree (device memory, 2 x spans items) in one launch.
-hipError_t launch_tree_items(const TreeItems *d_tree, uint32_t spans, hipStream_t s);
 
 // One-shot posts (ref.go:98-161 for one message of at most kMaxOneLen bytes:
 // a glfs.PostBlob of a small blob, a Writer's tail block, an index node of a

@@ -714,12 +714,9 @@ __device__ __forceinline__ void pair_pipelined(
 // next even block's before the odd one, so HBM latency is covered and no
 // buffer is copied on the loop back-edge.  Chunk-start / chunk-end flags and
 // the chaining-value reset are per-chunk (scalar), not per-block selects.
-// LAUX: cache policy of the staged loads (kLoadCoherent: device-coherent,
-// for bytes other XCDs wrote during the launch).  cst: bytes the staged
-// ctext stores may write from cmsg (0: none -- the stores fall outside the
-// buffer descriptor and are dropped; default: clen).
-constexpr uint32_t kLoadCoherent = 16;  // SC1 (gfx950 cache policy bits)
-template <int G, bool CHACHA, bool STAGE = false, int A = 2, uint32_t LAUX = 0>
+// cst: bytes the staged ctext stores may write from cmsg (0: none -- the
+// stores fall outside the buffer descriptor and are dropped; default: clen).
+template <int G, bool CHACHA, bool STAGE = false, int A = 2>
 __device__ __forceinline__ void lane_subtree_full(
     uint32_t (&cv)[8], const uint8_t *msg, uint8_t *cmsg, uint32_t first,
     bool whole, const uint32_t (&key)[8], uint32_t base,
@@ -769,7 +766,7 @@ __device__ __forceinline__ void lane_subtree_full(
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc_ld, (__attribute__((address_space(3))) void *)(uintptr_t)(sb + 1024u * k),
           16, (k & 1) ? (lo0 ^ 64u) : lo0, ((8u * k * uint32_t(G)) << 10) + 128u * s,
-          0, LAUX);
+          0, 0);
   };
   if constexpr (gl) issue(0);
   for (uint32_t jj = 0; jj < uint32_t(G); ++jj) {
@@ -2150,163 +2147,6 @@ __device__ __forceinline__ void small_fine(const SArgs &a, uint64_t b0, uint4 *l
   }
 }
 
-// ---- Tree items: the one-call config-4 route's tree blob (TreeItems) ----
-// Left-complete merge of the CVs of lanes [0, cnt) of the wave (lane l =
-// leaf l, cnt <= 64, uniform), ROOT on the top parent when `root`; the
-// result is in lane 0.  At stride st, lane l (l % 2st == 0) takes lane
-// l + st as its right child when that leaf exists, else passes through:
-// BLAKE3's tree (as tree_reduce).
-template <int A>
-__device__ __forceinline__ void wave_merge(uint32_t (&cv)[8], uint32_t cnt, bool root,
-                                           const uint32_t (&key)[8], uint32_t base) {
-  const uint32_t l = threadIdx.x & 63u;
-  for (uint32_t st = 1; st < cnt; st <<= 1) {
-    uint32_t m[16];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      m[w] = cv[w];
-      m[8 + w] = uint32_t(__shfl_down(int(cv[w]), st, 64));
-    }
-    if ((l & (2 * st - 1)) == 0 && l + st < cnt) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) cv[w] = key[w];
-      b3_compress<A>(cv, m, 0u, 0u, 64u,
-                     base | kParent | ((root && 2 * st >= cnt) ? kRoot : 0u));
-    }
-  }
-}
-
-// Tree item t (of 2 x spans) of k_tree_items: t < spans = the DEK item of
-// span t, else the CID item of span t - spans.  The whole wave runs it; lane
-// l hashes chunk l of the span.  A CID item waits (bounded by T->wait_ticks;
-// a timeout sets *err and the host discards the call's results) for its
-// block's DEK.
-template <int A>
-__device__ __forceinline__ void tree_item(const TreeItems *T, uint64_t t, uint4 *lds_u4) {
-  const uint32_t spans = T->spans, spb = T->spb;
-  const bool cid = t >= spans;
-  const uint32_t g = uint32_t(cid ? t - spans : t);
-  const uint32_t b = g / spb, s = g - b * spb;
-  const uint64_t total = T->total;
-  const uint64_t lo = uint64_t(g) * kTreeSpan;
-  const uint32_t slen = uint32_t(min<uint64_t>(kTreeSpan, total - lo));
-  const uint64_t blen = min<uint64_t>(T->bs, total - uint64_t(b) * T->bs);
-  const uint32_t W = uint32_t((blen + kTreeSpan - 1) / kTreeSpan);  // spans of block b
-  const uint32_t C = (slen + 1023) >> 10;                          // chunks of span g
-  const uint32_t l = threadIdx.x & 63u;
-  uint8_t *ref = T->refs + 64ull * b;
-  uint32_t key[8], dek[8];
-  uint32_t base;
-  if (cid) {
-    if (l == 0) {  // the block's DEK (published with its ready flag)
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(T->ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > T->wait_ticks) {
-          __hip_atomic_store(T->err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-    }
-    // the loads below stay after the wait (the flag was an agent-scope load)
-    __atomic_signal_fence(__ATOMIC_ACQUIRE);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      key[i] = T->cid_key[i];
-      dek[i] = __builtin_amdgcn_readfirstlane(
-          load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i));
-    }
-    base = T->cid_base;
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      key[i] = T->salt[i];
-      dek[i] = 0;
-    }
-    base = kKeyed;
-  }
-  const uint8_t *msg = T->lines + lo;
-  uint8_t *cmsg = T->ctext ? T->ctext + lo : nullptr;
-  uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (slen == kTreeSpan) {  // 64 full chunks: k_pass's staged lane layout (G = 1)
-    const uint32_t wl = lds_offset(lds_u4 + (threadIdx.x >> 6) * 512);
-    if (cid)  // (no ctext wanted: the staged stores fall outside a 0-byte descriptor)
-      lane_subtree_full<1, true, true, A>(cv, msg, cmsg ? cmsg : const_cast<uint8_t *>(msg), l,
-                                          false, key, base, dek, wl, uint32_t(kTreeSpan),
-                                          s * 64u, cmsg ? uint32_t(kTreeSpan) : 0u);
-    else
-      lane_subtree_full<1, false, true, A>(cv, msg, nullptr, l, false, key, base, dek, wl,
-                                           uint32_t(kTreeSpan), s * 64u);
-  } else if (l < C) {  // the blob's last span: chunk l of slen bytes
-    const bool one = W == 1 && C == 1;  // the chunk is the whole block
-    if (cid)
-      lane_subtree<1, true, true, A>(cv, msg, cmsg, slen, l, 1, one, key, base, dek, s * 64u);
-    else
-      lane_subtree<1, false, true, A>(cv, msg, nullptr, slen, l, 1, one, key, base, dek,
-                                      s * 64u);
-  }
-  wave_merge<A>(cv, C, W == 1, key, base);
-  uint32_t last = W == 1;
-  if (W > 1) {  // the span's CV; the block's last span to finish merges them
-    uint32_t *scv = cid ? T->cid_cv : T->dek_cv;
-    if (l == 0) {
-      publish_cv(scv + uint64_t(g) * 8, cv);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the CV stores are done
-      last = __hip_atomic_fetch_add((cid ? T->cid_cnt : T->dek_cnt) + b, 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == W;
-    }
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (last) {
-      if (l < W) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          cv[i] = load_cv_word(scv + (uint64_t(b) * spb + l) * 8 + i);
-      }
-      wave_merge<A>(cv, W, true, key, base);
-    }
-  }
-  if (last && l == 0) {
-    if (cid) {
-      store_digest(ref, cv);  // read by the next launch (the index node)
-    } else {
-      publish_cv(reinterpret_cast<uint32_t *>(ref + 32), cv);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (b != T->skip_block)
-        __hip_atomic_store(T->ready + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// The tree blob of the one-call config-4 route (TreeItems) after the blobs'
-// CID pass has written its lines: DEK items of the 64 KiB spans (one chunk
-// per lane), then their CID items, as many waves as the chip holds taking
-// items from a counter (bank epoch & 1 of two, the other zeroed by workgroup
-// 0 for the next launch on the stream).  A CID item only ever comes from the
-// counter, after every DEK item has been handed out to a running wave.
-template <int A>
-__global__ __launch_bounds__(256, 4) void k_tree_items(const TreeItems *T, uint32_t *ctr,
-                                                       uint32_t epoch) {
-  __shared__ uint4 lds_u4[4 * 512];
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(ctr + ((epoch + 1u) & 1u) * 32u, 0u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t *mine = ctr + (epoch & 1u) * 32u;
-  const uint32_t S = T->spans;
-  const uint32_t waves = gridDim.x * 4u;
-  const uint32_t tb = S > waves ? S : waves;  // CID items start here
-  uint32_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
-  while (item < tb + S) {  // wave-uniform
-    if (item < S)
-      tree_item<A>(T, item, lds_u4);
-    else if (item >= tb)
-      tree_item<A>(T, uint64_t(S) + (item - tb), lds_u4);
-    uint32_t t = 0;
-    if ((threadIdx.x & 63u) == 0)
-      t = __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    item = waves + uint32_t(__builtin_amdgcn_readfirstlane(t));
-  }
-}
-
 template <int G, bool CHACHA, int A = 2>
 __global__ __launch_bounds__(256) void k_small(SArgs a) {
   // 4 waves x 8 KiB staging image (same layout as k_pass's)
@@ -3052,13 +2892,6 @@ void fused_debug(uint32_t skip_msg, uint64_t wait_us) {
 
 uint64_t fused_timeouts() { return g_dc_timeouts.load(std::memory_order_relaxed); }
 
-void fused_debug_take(uint32_t *skip, uint64_t *wait_ticks) {
-  *skip = g_dc_skip_msg.exchange(~0u, std::memory_order_relaxed);
-  *wait_ticks = g_dc_wait_ticks.load(std::memory_order_relaxed);
-}
-
-void fused_timeout_add() { g_dc_timeouts.fetch_add(1, std::memory_order_relaxed); }
-
 void blake3_iv_words(uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) w[i] = kIV[i];
 }
@@ -3245,20 +3078,6 @@ hipError_t clock_probe(int reset, uint64_t out[2]) {
   if (!reset) return hipSuccess;
   const unsigned long long z[2] = {0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof z, 0, hipMemcpyHostToDevice);
-}
-
-hipError_t launch_tree_items(const TreeItems *d_tree, uint32_t spans, hipStream_t s) {
-  if (spans == 0) return hipSuccess;
-  static const uint32_t slots = resident_wgs(k_tree_items<GLFSX_SMALL_CID>);
-  uint32_t *ctr;
-  uint32_t epoch;
-  hipError_t e = small_q_get(s, &ctr, &epoch);
-  if (e != hipSuccess) return e;
-  const uint32_t wgs = (2 * spans + 3) / 4;
-  const uint32_t grid = std::min(wgs, slots ? slots : wgs);
-  hipLaunchKernelGGL(k_tree_items<GLFSX_SMALL_CID>, dim3(grid), dim3(256), 0, s, d_tree, ctr,
-                     epoch);
-  return hipGetLastError();
 }
 
 #if GLFSX_WGTIME

@@ -111,12 +111,9 @@ uint32_t glfsx_set_latency_wgs(uint32_t wgs);
  * workgroups runs both passes in one launch, each CID work item waiting for
  * its block's DEK; a wait that exceeds its bound fails the launch loudly:
  * the calls that synchronise repeat the post with two launches (Create,
- * post_batch, the Writer) and count it.  glfsx_post_tree_device's tree
- * items (the tree blob's 64 KiB spans as the work items of one launch, CID
- * items waiting for their block's DEK) wait the same way, and the call is
- * then repeated with the general post of the tree blob.
+ * post_batch, the Writer) and count it.
  * glfsx_debug_fused makes the next such launch leave block skip_msg's DEK
- * unpublished (~0u: none; for tree items: tree block skip_msg) and sets the
+ * unpublished (~0u: none) and sets the
  * bound to wait_us microseconds (0: the default, 1 s).  Returns the number
  * of failed one-launch posts seen so far, process-wide. */
 uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);

@@ -429,12 +429,10 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
 @pytest.mark.parametrize("n,tree_bs", [(70_000, 2 * MIB), (3000, 4096), (300, 64 * 1024),
                                        (1, 2 * MIB), (257, 1024),
                                        # one tree block at 8 MiB (its ref is
-                                       # the root; no tree items: > 64 spans);
-                                       # 5 blocks + an index node
+                                       # the root); 5 blocks + an index node
                                        (20_000, 8 * MIB), (20_000, MIB),
-                                       # 64 spans per block (the most tree
-                                       # items take), 3 blocks; 2 spans per
-                                       # block, the last span partial
+                                       # 3 blocks; 2 x 64 KiB per block, the
+                                       # last one partial
                                        (40_000, 4 * MIB), (2_500, 128 * 1024)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
     """glfsx_post_tree_device (blob hashing and tree lines overlapped; tree
@@ -585,66 +583,3 @@ def test_post_tree_device_keyed_cid_and_ctext(gpu, O):
                                         .tobytes()), 2 * MIB, salt=bsalt, cid_key=key,
                                   closed_form=True)
     assert bytes(roots2[64 * i:64 * i + 64].cpu().numpy().tobytes()) == want_root
-
-
-def test_post_tree_device_tree_item_timeout_repeats(gpu, O):
-    """A tree item that gives up waiting must not fail silently: block 1's
-    DEK is withheld from its CID items (glfsx_debug_fused), they time out
-    after 2 ms, and the call is repeated with the general post of the tree
-    blob -- same roots, lines and tree root as the three calls, one failure
-    counted; the next call (no fault) is clean."""
-    import ctypes
-    import torch
-    from glfs_amd import _native as N
-    n, tree_bs = 20_000, MIB
-    lens_h = [(i * 37) % 9000 for i in range(n)]
-    offs_h, o = [], 0
-    for ln in lens_h:
-        offs_h.append(o)
-        o += ln
-    data = torch.empty(o + 64, dtype=torch.uint8, device="cuda")
-    N.check(N.lib.glfsx_fill_splitmix_device(data.data_ptr(), 0, o + 8 - o % 8, 5, None))
-    names = [b"t%06d" % i for i in range(n)]
-    offs = torch.tensor(offs_h, dtype=torch.int64, device="cuda")
-    lens = torch.tensor(lens_h, dtype=torch.int64, device="cuda")
-    dn, dno, dm, dt, dto, _, dbs = _tree_inputs(torch, names, [b"blob"] * n, [0o644] * n,
-                                                lens_h, [2 * MIB] * n)
-    bsalt, tsalt = O.derive_key(bytes(32), b"blob"), O.derive_key(bytes(32), b"tree")
-    cap = 300 * n
-    roots1 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
-    N.check(N.lib.glfsx_post_blobs_device(2 * MIB, bsalt, None, data.data_ptr(), offs.data_ptr(),
-                                          lens.data_ptr(), n, 16384, None, roots1.data_ptr(),
-                                          None))
-    out1 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-    t1 = ctypes.c_uint64()
-    N.check(N.lib.glfsx_tree_encode_device(n, dn.data_ptr(), dno.data_ptr(), dm.data_ptr(),
-                                           dt.data_ptr(), dto.data_ptr(), roots1.data_ptr(),
-                                           lens.data_ptr(), dbs.data_ptr(), out1.data_ptr(),
-                                           cap, None, ctypes.byref(t1), None))
-    r1 = N.glfsx_root()
-    N.check(N.lib.glfsx_create_device(tree_bs, tsalt, None, out1.data_ptr(), t1.value, None,
-                                      ctypes.byref(r1), None, None))
-    assert t1.value > 2 * tree_bs   # block 1 exists
-
-    def one_call():
-        roots2 = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
-        out2 = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-        r2, t2 = N.glfsx_root(), ctypes.c_uint64()
-        N.check(N.lib.glfsx_post_tree_device(n, 2 * MIB, bsalt, tsalt, None, data.data_ptr(),
-                                             offs.data_ptr(), lens.data_ptr(), 9000, None,
-                                             roots2.data_ptr(), dn.data_ptr(), dno.data_ptr(),
-                                             dm.data_ptr(), dt.data_ptr(), dto.data_ptr(),
-                                             dbs.data_ptr(), tree_bs, out2.data_ptr(), cap,
-                                             None, ctypes.byref(r2), ctypes.byref(t2), None))
-        torch.cuda.synchronize()
-        assert t2.value == t1.value and bytes(r2.ref) == bytes(r1.ref)
-        assert torch.equal(roots1, roots2) and torch.equal(out1[:t1.value], out2[:t1.value])
-
-    try:
-        before = N.lib.glfsx_debug_fused(1, 2000)
-        one_call()                                        # fault, repeated
-        assert N.lib.glfsx_debug_fused(0xFFFFFFFF, 0) == before + 1
-        one_call()                                        # clean
-        assert N.lib.glfsx_debug_fused(0xFFFFFFFF, 0) == before + 1
-    finally:
-        N.lib.glfsx_debug_fused(0xFFFFFFFF, 0)
