@@ -1385,6 +1385,45 @@ __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
   b ^= d;
 }
 
+// The latency kernels' form (k_quad, k_one, k_med_*): the 28 words first,
+// then the rounds.  quad_compress's per-round reads put an LDS round trip in
+// front of nearly every G step (the scheduler keeps ~4 reads in flight, the
+// dependent chain covers ~6 instructions of each): a one-wave compression
+// measured 0.78 us.  Callers issue the next block's words before the
+// current compression (sched_barrier fences), so the chain never waits.
+__device__ __forceinline__ void quad_load(uint32_t (&m)[28], const uint32_t (&addr)[28],
+                                          uint32_t off) {
+#pragma unroll
+  for (int k = 0; k < 28; ++k)
+    m[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[k] + off);
+}
+
+__device__ __forceinline__ void quad_compress_m(uint32_t &a, uint32_t &b, uint32_t c,
+                                                uint32_t d, const uint32_t (&m)[28]) {
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    QG(a, b, c, d, m[4 * r], m[4 * r + 1]);
+    b = qrot1(b);
+    c = qrot2(c);
+    d = qrot3(d);
+    QG(a, b, c, d, m[4 * r + 2], m[4 * r + 3]);
+    b = qrot3(b);
+    c = qrot2(c);
+    d = qrot1(d);
+  }
+  a ^= c;
+  b ^= d;
+}
+
+// One compression of the 64-B slot at addr (all reads before the rounds).
+__device__ __forceinline__ void quad_compress_pre(uint32_t &a, uint32_t &b, uint32_t c,
+                                                  uint32_t d, const uint32_t (&addr)[28]) {
+  uint32_t m[28];
+  quad_load(m, addr, 0u);
+  __builtin_amdgcn_sched_barrier(0);
+  quad_compress_m(a, b, c, d, m);
+}
+
 __device__ __forceinline__ uint32_t qsel(uint32_t q, uint32_t x0, uint32_t x1,
                                          uint32_t x2, uint32_t x3) {
   return q == 0 ? x0 : q == 1 ? x1 : q == 2 ? x2 : x3;
@@ -1468,7 +1507,10 @@ __device__ __forceinline__ void tree_reduce_q(uint32_t *lds, uint32_t k, uint32_
 // CUs instead of 8).
 template <int QPW>
 __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
-  __shared__ uint4 slots[QPW * 4];      // 64 B message slot per quad
+  // two 64-B message slots per quad (blocks alternate, so the next block is
+  // staged and read while this one is compressed); the merge uses the
+  // first QPW x 64 B as one slot per parent
+  __shared__ uint4 slots[QPW * 8];
   __shared__ uint32_t passbuf[8];       // the odd subtree passing up a level
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint64_t j = blockIdx.x >> a.split_log2;
@@ -1507,12 +1549,40 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
         blk[b] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
+    // QPW <= 64 (latency launches, up to 512 VGPRs per lane): block b in
+    // slot b & 1, staged and its words read one block ahead (one wave's LDS
+    // accesses complete in order; slot b & 1 was last read for block b - 2,
+    // whose words were consumed by its compression).  QPW = 256 (four
+    // waves per SIMD, 128 VGPRs beside the 16 staged blocks): one slot and
+    // quad_compress's per-round reads, as before.
+    const uint32_t bslot = lds_offset(slots + quad * 8);
+    uint32_t baddr[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) baddr[k] = addr[k] - slot + bslot;
+    uint32_t m[28];
+    if constexpr (QPW <= 64) {
+      *reinterpret_cast<lds_u32x4 *>(bslot + 16u * q) =
+          u32x4{blk[0].x, blk[0].y, blk[0].z, blk[0].w};
+      quad_load(m, baddr, 0u);
+    }
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
-        *reinterpret_cast<lds_u32x4 *>(slot + 16u * q) =
-            u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t nx[28];
+        const bool more = QPW <= 64 && b + 1 < 16 && uint32_t(b + 1) < nb;
+        if constexpr (QPW <= 64) {
+          if (more) {
+            const uint32_t o = 64u * uint32_t((b + 1) & 1);
+            *reinterpret_cast<lds_u32x4 *>(bslot + o + 16u * q) =
+                u32x4{blk[(b + 1) & 15].x, blk[(b + 1) & 15].y, blk[(b + 1) & 15].z,
+                      blk[(b + 1) & 15].w};
+            quad_load(nx, baddr, o);
+          }
+        } else {
+          *reinterpret_cast<lds_u32x4 *>(bslot + 16u * q) =
+              u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = a.base;
         if (b == 0) fl |= kChunkStart;
@@ -1521,9 +1591,19 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
           if (whole && cnt == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr, 0u, blen, fl);
-        quad_compress(cl, ch, ivq, dq, addr);
-        // the slot is rewritten next block: reads of this block are done
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (QPW <= 64) {
+          __builtin_amdgcn_sched_barrier(0);
+          quad_compress_m(cl, ch, ivq, dq, m);
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          quad_compress(cl, ch, ivq, dq, baddr);
+          // the slot is rewritten next block: reads of this block are done
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if (more) {
+#pragma unroll
+          for (int k = 0; k < 28; ++k) m[k] = nx[k];
+        }
       }
     }
   }
@@ -1548,7 +1628,7 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
       cl = kq_lo;
       ch = kq_hi;
       const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
-      quad_compress(cl, ch, ivq, dq, addr);
+      quad_compress_pre(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
@@ -1604,7 +1684,7 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
       cl = kq_lo;
       ch = kq_hi;
       const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
-      quad_compress(cl, ch, ivq, dq, addr);
+      quad_compress_pre(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
@@ -1647,9 +1727,14 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
     uint32_t addr[28];
 #pragma unroll
     for (int k = 0; k < 28; ++k) addr[k] = img + (quad << 10) + rel[k];
+    uint32_t m[28];  // block b's words, read while block b - 1 is compressed
+    quad_load(m, addr, 0u);
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
+        uint32_t nx[28];
+        const bool more = b + 1 < 16 && uint32_t(b + 1) < nb;
+        if (more) quad_load(nx, addr, 64u * uint32_t(b + 1));
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = base;
         if (b == 0) fl |= kChunkStart;
@@ -1658,10 +1743,13 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
           if (root && C == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr0 + quad, 0u, blen, fl);
-        uint32_t ab[28];
+        __builtin_amdgcn_sched_barrier(0);
+        quad_compress_m(cl, ch, ivq, dq, m);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) {
 #pragma unroll
-        for (int k = 0; k < 28; ++k) ab[k] = addr[k] + 64u * b;
-        quad_compress(cl, ch, ivq, dq, ab);
+          for (int k = 0; k < 28; ++k) m[k] = nx[k];
+        }
       }
     }
   }
@@ -1698,7 +1786,7 @@ __device__ __forceinline__ void one_tree(uint32_t &cl, uint32_t &ch, uint32_t co
       uint32_t addr[28];
 #pragma unroll
       for (int k = 0; k < 28; ++k) addr[k] = ts + (quad << 6) + rel[k];
-      quad_compress(cl, ch, ivq, dq, addr);
+      quad_compress_pre(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
@@ -1728,22 +1816,36 @@ __device__ __forceinline__ void one_hash(uint32_t &cl, uint32_t &ch, uint32_t im
 // 64-B block (one block when empty): bytes at and past `present` read as
 // zero (an index node posted from its refs alone).  dcopy (nullable): the
 // staged image is also stored there (the medium path's device copy).
+// Every lane's loads are issued before any is waited for: the source is
+// the caller's pinned staging, one PCIe round trip (~1.7 us) per wave of
+// loads, which a loop that waits per iteration paid 4x at 4 KiB and 16x at
+// 16 KiB.  padded <= 16 x LANES x 16 B (k_one<16>: 16 KiB, k_one<64> and a
+// k_med span: 64 KiB).
 template <int LANES>
 __device__ __forceinline__ void one_stage(uint4 *img_u4, const uint8_t *src, uint32_t len,
                                           uint32_t present, uint8_t *dcopy) {
   const uint32_t padded = len ? (len + 63) & ~63u : 64u;
   const uint32_t have = min(len, present);
-  for (uint32_t p = threadIdx.x * 16u; p < padded; p += LANES * 16u) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (p + 16u <= have) {
-      v = *reinterpret_cast<const uint4 *>(src + p);
-    } else if (p < have) {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t i = 0; p + i < have; ++i) w[i >> 2] |= uint32_t(src[p + i]) << (8 * (i & 3));
-      v = make_uint4(w[0], w[1], w[2], w[3]);
+  constexpr int IT = 16;
+  uint4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const uint32_t p = (threadIdx.x + uint32_t(i) * LANES) * 16u;
+    v[i] = make_uint4(0, 0, 0, 0);
+    if (p + 16u <= have) v[i] = *reinterpret_cast<const uint4 *>(src + p);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const uint32_t p = (threadIdx.x + uint32_t(i) * LANES) * 16u;
+    if (p < padded) {
+      if (p < have && p + 16u > have) {  // the one partial granule
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; p + k < have; ++k) w[k >> 2] |= uint32_t(src[p + k]) << (8 * (k & 3));
+        v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      img_u4[p >> 4] = v[i];
+      if (dcopy) *reinterpret_cast<uint4 *>(dcopy + p) = v[i];
     }
-    img_u4[p >> 4] = v;
-    if (dcopy) *reinterpret_cast<uint4 *>(dcopy + p) = v;
   }
 }
 
@@ -1796,8 +1898,29 @@ __device__ __forceinline__ void one_signal(const OneDesc *dp) {
     __hip_atomic_store(dp->flag, dp->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Phase timing of k_one (A/B variant builds only: GLFSX_ONE_TIMING=1,
+// scripts/one_trace.py): workgroup 0 adds s_memrealtime ticks since its
+// start at each phase boundary.
+#if GLFSX_ONE_TIMING
+__device__ unsigned long long g_one_t[16];
+#define ONE_T(i)                                                                        \
+  do {                                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                            \
+      __hip_atomic_fetch_add(&g_one_t[i],                                               \
+                             (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0), \
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);               \
+  } while (0)
+#else
+#define ONE_T(i) \
+  do {           \
+  } while (0)
+#endif
+
 template <int QUADS>
 __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
+#if GLFSX_ONE_TIMING
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
   __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
   __shared__ uint32_t passbuf[8];
@@ -1807,10 +1930,12 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
   const uint32_t len = dp->len;
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
+  ONE_T(0);
   one_stage<kLanes>(img_u4, dp->src, len, dp->present, nullptr);
   uint32_t rel[28];
   quad_addrs(rel, 0u, q);
   __syncthreads();
+  ONE_T(1);
   uint32_t key[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
@@ -1821,11 +1946,13 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
     s_dek[4 + q] = ch;
   }
   __syncthreads();
+  ONE_T(2);
   uint32_t dek[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) dek[i] = s_dek[i];
   one_xor<kLanes>(img_u4, len, dek, 0u);
   __syncthreads();
+  ONE_T(3);
   if (dp->ctext) one_store<kLanes>(img_u4, dp->ctext, len);  // drains during the CID
   uint32_t ckey[8];
 #pragma unroll
@@ -1838,7 +1965,13 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
     r[8 + q] = dek[q];
     r[12 + q] = dek[4 + q];
   }
+  ONE_T(4);
   one_signal(dp);
+  ONE_T(5);
+#if GLFSX_ONE_TIMING
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(&g_one_t[15], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // ---- Medium one-shot posts (kMaxOneLen < len <= kMaxMedLen) ----
@@ -1926,8 +2059,19 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
   const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
   // the device copy holds the span zero padded to 64 B (k_med_dek)
   const uint32_t padded = (slen + 63) & ~63u;
-  for (uint32_t p = tid * 16u; p < padded; p += 256 * 16u)
-    img_u4[p >> 4] = *reinterpret_cast<const uint4 *>(dp->dmsg + off + p);
+  {
+    uint4 v[16];  // all loads in flight at once (see one_stage)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t p = (tid + uint32_t(i) * 256u) * 16u;
+      if (p < padded) v[i] = *reinterpret_cast<const uint4 *>(dp->dmsg + off + p);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t p = (tid + uint32_t(i) * 256u) * 16u;
+      if (p < padded) img_u4[p >> 4] = v[i];
+    }
+  }
   uint32_t dek[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) dek[i] = dp->dek[i];
@@ -3066,6 +3210,18 @@ hipError_t launch_post_small(const SmallJob &job, hipStream_t s) {
   }
   return launch_small_pass<true>(a, max_len, s);
 }
+
+#if GLFSX_ONE_TIMING
+extern "C" int glfsx_debug_one_timing(int reset, uint64_t out[16]) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_one_t), 16 * sizeof(uint64_t), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (!reset) return 0;
+  const unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_one_t), z, sizeof z, 0, hipMemcpyHostToDevice) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t clock_probe(int reset, uint64_t out[2]) {
   unsigned long long v[2] = {0, 0};

@@ -1,1 +1,7 @@
-bash scripts/gpu_round_check.sh r5c && for leg in config4all config2; do timeout -k 10 300 python -u scripts/legs.py $leg >> gpurun_out/r5c_${leg}.json 2> gpurun_out/r5c_${leg}.err || exit 1; done && echo legs ok
+export TMPDIR=/tmp
+bash scripts/gpu_round_check.sh r5d || exit 1
+for r in 1 2; do
+  GLFSX_LIB=$PWD/glfs_amd/libglfsx_base.so timeout -k 10 200 python scripts/legs.py postblob > gpurun_out/r5d_pb_base_$r.json || exit 1
+  timeout -k 10 200 python scripts/legs.py postblob > gpurun_out/r5d_pb_new_$r.json || exit 1
+done
+echo legs ok
