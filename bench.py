@@ -1363,17 +1363,24 @@ def postblob_concurrency(N, ln=4096, plan=((1, 3000), (16, 1500), (64, 600), (25
     import torch
     dev = int(torch.cuda.current_device())
     res = {}
+    stats = (ctypes.c_uint64 * 3)()
     for threads, calls in plan:
         out = (ctypes.c_double * 5)()
+        N.check(N.lib.glfsx_one_stats(1, None))
         rc = lib.postbench_run(*fns, threads, ln, calls, salt, dev, out)
         N.check(rc, "postbench")
+        N.check(N.lib.glfsx_one_stats(1, stats))
         res[str(threads)] = {"calls_per_s": round(out[0] / out[1]), "calls": int(out[0]),
                              "p50_us": round(out[2], 1), "p90_us": round(out[3], 1),
-                             "p99_us": round(out[4], 1)}
+                             "p99_us": round(out[4], 1), "launches": int(stats[0]),
+                             "mean_batch": round(stats[1] / max(stats[0], 1), 2),
+                             "lanes_full": int(stats[2])}
     return {"by_threads": res, "blob_bytes": ln,
             "what": "concurrent glfs.PostBlob of distinct 4 KiB blobs: T C threads each calling "
                     "glfsx_create back to back (bs 2 MiB, blob type salt, counting sink); "
-                    "calls_per_s = calls / wall time, latency percentiles per call"}
+                    "calls_per_s = calls / wall time, latency percentiles per call; launches / "
+                    "mean_batch / lanes_full from glfsx_one_stats (group commit: requests per "
+                    "launch, leader found all 8 launch lanes busy), warm-up calls included"}
 
 
 def concat_leg(N, bs=MIB, size=GIB):

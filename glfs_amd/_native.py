@@ -70,6 +70,7 @@ SIGNATURES = {
     "glfsx_set_latency_wgs": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_debug_fused": (_U64, [ctypes.c_uint32, _U64]),
     "glfsx_clock_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+    "glfsx_one_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),
     "glfsx_post": (_INT, [_CP, _VP, _U64, _VP, _VP, _CP]),
     "glfsx_post_batch": (_INT, [_CP, _VP, _U64, _U64, _VP, _VP, _CP]),

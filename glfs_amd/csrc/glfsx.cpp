@@ -21,6 +21,7 @@
 #include <cerrno>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 #include <string>
 #include <thread>
@@ -284,8 +285,11 @@ struct OnePoster {
   // leader takes it whole)
   std::atomic<OneReq *> pending{nullptr};
   std::atomic<bool> leader{false};
+  std::atomic<int> spinners{0};  // callers polling their flag without sleeping
   OneLane lane[kOneLanes];
 };
+// glfsx_one_stats: launches, requests launched, lane-full events
+std::atomic<uint64_t> g_one_stats[3];
 constexpr int kMaxPosterDevs = 64;
 std::mutex g_posters_mu;                               // creation only
 std::atomic<OnePoster *> g_posters[kMaxPosterDevs];    // one per device, process lifetime
@@ -391,6 +395,21 @@ bool one_finished(const OneReq *r) {
   return int32_t(v - r->seq) >= 0;
 }
 
+const int kOneSpinners = [] {
+  const int h = int(std::thread::hardware_concurrency());
+  return std::min(16, std::max(4, h / 2));
+}();
+constexpr int64_t kOneSpinNs = 300000;
+// A sleeping waiter's 10 us sleeps would otherwise end up to the default
+// 50 us timer slack late: once per thread, its slack is set to 1 us.
+void one_sleep_slack() {
+  static thread_local bool set = [] {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+    return true;
+  }();
+  (void)set;
+}
+
 // Post rs[0..n) on device dev (the calling thread's current device); returns
 // when every request's ctext and ref are in its staging.
 int one_post_many(int dev, OneReq *const *rs, size_t n) {
@@ -400,6 +419,23 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
   OnePoster *P;
   if (int e = poster_get(dev, &P)) return e;
   for (size_t i = 0; i < n; ++i) pending_push(P, rs[i]);
+  // Waiting: at most kOneSpinners callers (half the host's threads, 4-16)
+  // poll with `pause` (a post is ~45-190 us; up to kOneSpinNs); the others,
+  // and a spinner past that bound, sleep between polls.  Yielding instead (round 4) kept
+  // every waiting caller runnable: at 64-256 callers on a 16-core share
+  // the callers that had work (the leader, a caller whose post finished)
+  // waited for a core.
+  bool spin = P->spinners.fetch_add(1, std::memory_order_relaxed) < kOneSpinners;
+  if (!spin) P->spinners.fetch_sub(1, std::memory_order_relaxed);
+  struct Unspin {
+    OnePoster *P;
+    bool &spin;
+    ~Unspin() {
+      if (spin) P->spinners.fetch_sub(1, std::memory_order_relaxed);
+    }
+  } unspin{P, spin};
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t sleeps = 0;
   size_t ndone = 0;  // rs[0..ndone) are finished or failed
   for (uint32_t spins = 0;; ++spins) {
     while (ndone < n && (rs[ndone]->done.load(std::memory_order_acquire) ||
@@ -431,6 +467,7 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         break;
       }
       std::vector<OneReq *> batch;
+      if (!L) g_one_stats[2].fetch_add(1, std::memory_order_relaxed);
       if (L) {
         // up to kOneBatch requests, at most kMedBatchBytes of medium ones
         // (always at least one request); the rest goes back on the stack
@@ -454,6 +491,8 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         const uint32_t seq = ++L->seq;
         if (!rc) rc = one_launch(*L, batch, seq);
         if (!rc) {
+          g_one_stats[0].fetch_add(1, std::memory_order_relaxed);
+          g_one_stats[1].fetch_add(batch.size(), std::memory_order_relaxed);
           L->busy = true;
           for (size_t k = 0; k < batch.size(); ++k) {
             batch[k]->flag = L->h_flag + k;
@@ -476,12 +515,25 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
       P->leader.store(false, std::memory_order_release);
       continue;
     }
-    if (spins < 20000) {
+    if (spin) {
+      if ((spins & 31) != 0) {
+        for (int k = 0; k < 8; ++k) __builtin_ia32_pause();
+        continue;
+      }
+      // every 32 polls: the core goes to any runnable thread (the HIP
+      // runtime's own, a caller with work), and the spin bound is checked
       sched_yield();
-      continue;
+      if (std::chrono::duration_cast<std::chrono::nanoseconds>(
+              std::chrono::steady_clock::now() - t0).count() < kOneSpinNs)
+        continue;
+      spin = false;
+      P->spinners.fetch_sub(1, std::memory_order_relaxed);
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
-    if (spins % 1024 == 0) {
+    // sleepers back off 10 -> 40 us: hundreds of them must not wake 100 k
+    // times a second each
+    one_sleep_slack();
+    std::this_thread::sleep_for(std::chrono::microseconds(10u << std::min(sleeps, 2u)));
+    if (++sleeps % 1024 == 0) {
       // a long wait: a launch that failed on the device never sets its flags
       for (size_t i = ndone; i < n; ++i) {
         const OneReq *r = rs[i];
@@ -1465,6 +1517,15 @@ uint32_t glfsx_set_latency_wgs(uint32_t wgs) { return set_latency_wgs(wgs); }
 uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us) {
   fused_debug(skip_msg, wait_us);
   return fused_timeouts();
+}
+
+int glfsx_one_stats(int reset, uint64_t out[3]) {
+  for (int i = 0; i < 3; ++i) {
+    const uint64_t v = reset ? g_one_stats[i].exchange(0, std::memory_order_relaxed)
+                             : g_one_stats[i].load(std::memory_order_relaxed);
+    if (out) out[i] = v;
+  }
+  return 0;
 }
 
 int glfsx_clock_probe(int reset, uint64_t out[2]) {

@@ -127,6 +127,13 @@ uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);
  * after reading.  out may be NULL. */
 int glfsx_clock_probe(int reset, uint64_t out[2]);
 
+/* Measurement hook (no reference counterpart): the one-shot poster's
+ * process-wide counters since the last reset -- out[0] launches, out[1]
+ * requests they carried (out[1] / out[0] = the mean group-commit batch),
+ * out[2] times a leader found every launch lane busy.  reset != 0 zeroes
+ * them after reading.  out may be NULL. */
+int glfsx_one_stats(int reset, uint64_t out[3]);
+
 /* --- primitives -------------------------------------------------------- */
 /* ref.go:152 DeriveKey: BLAKE3 keyed with salt over input (any length),
  * the first out_len bytes of the XOF (any length; blake3.New(len(out), salt)
