@@ -117,6 +117,39 @@ def test_concurrent_one_shot_posts(gpu, O):
     assert not errors, errors[:5]
 
 
+def test_many_waiters_one_stats(gpu, O):
+    """64 threads posting small messages at once: more callers than the
+    poster lets spin (the rest sleep between polls), so sleepers, spinners
+    and leaders mix; every result == the oracle, and glfsx_one_stats counts
+    every request once (launches <= requests)."""
+    from glfs_amd import _native as N
+    N.check(N.lib.glfsx_one_stats(1, None))
+    errors = []
+    per, threads = 25, 64
+
+    def worker(t):
+        try:
+            N.check(N.lib.glfsx_set_device(0))
+            rng = random.Random(5000 + t)
+            for _ in range(per):
+                n = rng.choice([0, 9, 100, 4096, 5000, 16384])
+                salt = rng.randbytes(32)
+                data = rng.randbytes(n)
+                if _gpu_post(N, salt, data) != O.post(salt, data):
+                    errors.append((t, n))
+        except Exception as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+    st = (ctypes.c_uint64 * 3)()
+    N.check(N.lib.glfsx_one_stats(0, st))
+    assert st[1] == per * threads
+    assert 1 <= st[0] <= st[1]
+
+
 def test_concurrent_small_creates(gpu, O):
     """glfs.PostBlob-shaped calls (glfsx_create, one Writer per blob) from 12
     threads, with the blob type salt: roots == the oracle's Create."""
