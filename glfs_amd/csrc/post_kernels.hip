@@ -1385,45 +1385,6 @@ __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
   b ^= d;
 }
 
-// The latency kernels' form (k_quad, k_one, k_med_*): the 28 words first,
-// then the rounds.  quad_compress's per-round reads put an LDS round trip in
-// front of nearly every G step (the scheduler keeps ~4 reads in flight, the
-// dependent chain covers ~6 instructions of each): a one-wave compression
-// measured 0.78 us.  Callers issue the next block's words before the
-// current compression (sched_barrier fences), so the chain never waits.
-__device__ __forceinline__ void quad_load(uint32_t (&m)[28], const uint32_t (&addr)[28],
-                                          uint32_t off) {
-#pragma unroll
-  for (int k = 0; k < 28; ++k)
-    m[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[k] + off);
-}
-
-__device__ __forceinline__ void quad_compress_m(uint32_t &a, uint32_t &b, uint32_t c,
-                                                uint32_t d, const uint32_t (&m)[28]) {
-#pragma unroll
-  for (int r = 0; r < 7; ++r) {
-    QG(a, b, c, d, m[4 * r], m[4 * r + 1]);
-    b = qrot1(b);
-    c = qrot2(c);
-    d = qrot3(d);
-    QG(a, b, c, d, m[4 * r + 2], m[4 * r + 3]);
-    b = qrot3(b);
-    c = qrot2(c);
-    d = qrot1(d);
-  }
-  a ^= c;
-  b ^= d;
-}
-
-// One compression of the 64-B slot at addr (all reads before the rounds).
-__device__ __forceinline__ void quad_compress_pre(uint32_t &a, uint32_t &b, uint32_t c,
-                                                  uint32_t d, const uint32_t (&addr)[28]) {
-  uint32_t m[28];
-  quad_load(m, addr, 0u);
-  __builtin_amdgcn_sched_barrier(0);
-  quad_compress_m(a, b, c, d, m);
-}
-
 __device__ __forceinline__ uint32_t qsel(uint32_t q, uint32_t x0, uint32_t x1,
                                          uint32_t x2, uint32_t x3) {
   return q == 0 ? x0 : q == 1 ? x1 : q == 2 ? x2 : x3;
@@ -1507,10 +1468,7 @@ __device__ __forceinline__ void tree_reduce_q(uint32_t *lds, uint32_t k, uint32_
 // CUs instead of 8).
 template <int QPW>
 __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
-  // two 64-B message slots per quad (blocks alternate, so the next block is
-  // staged and read while this one is compressed); the merge uses the
-  // first QPW x 64 B as one slot per parent
-  __shared__ uint4 slots[QPW * 8];
+  __shared__ uint4 slots[QPW * 4];      // 64 B message slot per quad
   __shared__ uint32_t passbuf[8];       // the odd subtree passing up a level
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint64_t j = blockIdx.x >> a.split_log2;
@@ -1549,40 +1507,12 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
         blk[b] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
-    // QPW <= 64 (latency launches, up to 512 VGPRs per lane): block b in
-    // slot b & 1, staged and its words read one block ahead (one wave's LDS
-    // accesses complete in order; slot b & 1 was last read for block b - 2,
-    // whose words were consumed by its compression).  QPW = 256 (four
-    // waves per SIMD, 128 VGPRs beside the 16 staged blocks): one slot and
-    // quad_compress's per-round reads, as before.
-    const uint32_t bslot = lds_offset(slots + quad * 8);
-    uint32_t baddr[28];
-#pragma unroll
-    for (int k = 0; k < 28; ++k) baddr[k] = addr[k] - slot + bslot;
-    uint32_t m[28];
-    if constexpr (QPW <= 64) {
-      *reinterpret_cast<lds_u32x4 *>(bslot + 16u * q) =
-          u32x4{blk[0].x, blk[0].y, blk[0].z, blk[0].w};
-      quad_load(m, baddr, 0u);
-    }
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
-        uint32_t nx[28];
-        const bool more = QPW <= 64 && b + 1 < 16 && uint32_t(b + 1) < nb;
-        if constexpr (QPW <= 64) {
-          if (more) {
-            const uint32_t o = 64u * uint32_t((b + 1) & 1);
-            *reinterpret_cast<lds_u32x4 *>(bslot + o + 16u * q) =
-                u32x4{blk[(b + 1) & 15].x, blk[(b + 1) & 15].y, blk[(b + 1) & 15].z,
-                      blk[(b + 1) & 15].w};
-            quad_load(nx, baddr, o);
-          }
-        } else {
-          *reinterpret_cast<lds_u32x4 *>(bslot + 16u * q) =
-              u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
+        *reinterpret_cast<lds_u32x4 *>(slot + 16u * q) =
+            u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = a.base;
         if (b == 0) fl |= kChunkStart;
@@ -1591,19 +1521,9 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
           if (whole && cnt == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr, 0u, blen, fl);
-        if constexpr (QPW <= 64) {
-          __builtin_amdgcn_sched_barrier(0);
-          quad_compress_m(cl, ch, ivq, dq, m);
-          __builtin_amdgcn_sched_barrier(0);
-        } else {
-          quad_compress(cl, ch, ivq, dq, baddr);
-          // the slot is rewritten next block: reads of this block are done
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        if (more) {
-#pragma unroll
-          for (int k = 0; k < 28; ++k) m[k] = nx[k];
-        }
+        quad_compress(cl, ch, ivq, dq, addr);
+        // the slot is rewritten next block: reads of this block are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
     }
   }
@@ -1628,7 +1548,7 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
       cl = kq_lo;
       ch = kq_hi;
       const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
-      quad_compress_pre(cl, ch, ivq, dq, addr);
+      quad_compress(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
@@ -1684,7 +1604,7 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
       cl = kq_lo;
       ch = kq_hi;
       const uint32_t dq = qsel(q, 0u, 0u, 64u, fl);
-      quad_compress_pre(cl, ch, ivq, dq, addr);
+      quad_compress(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
@@ -1727,14 +1647,9 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
     uint32_t addr[28];
 #pragma unroll
     for (int k = 0; k < 28; ++k) addr[k] = img + (quad << 10) + rel[k];
-    uint32_t m[28];  // block b's words, read while block b - 1 is compressed
-    quad_load(m, addr, 0u);
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
-        uint32_t nx[28];
-        const bool more = b + 1 < 16 && uint32_t(b + 1) < nb;
-        if (more) quad_load(nx, addr, 64u * uint32_t(b + 1));
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = base;
         if (b == 0) fl |= kChunkStart;
@@ -1743,13 +1658,10 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
           if (root && C == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr0 + quad, 0u, blen, fl);
-        __builtin_amdgcn_sched_barrier(0);
-        quad_compress_m(cl, ch, ivq, dq, m);
-        __builtin_amdgcn_sched_barrier(0);
-        if (more) {
+        uint32_t ab[28];
 #pragma unroll
-          for (int k = 0; k < 28; ++k) m[k] = nx[k];
-        }
+        for (int k = 0; k < 28; ++k) ab[k] = addr[k] + 64u * b;
+        quad_compress(cl, ch, ivq, dq, ab);
       }
     }
   }
@@ -1786,7 +1698,7 @@ __device__ __forceinline__ void one_tree(uint32_t &cl, uint32_t &ch, uint32_t co
       uint32_t addr[28];
 #pragma unroll
       for (int k = 0; k < 28; ++k) addr[k] = ts + (quad << 6) + rel[k];
-      quad_compress_pre(cl, ch, ivq, dq, addr);
+      quad_compress(cl, ch, ivq, dq, addr);
     } else if (odd && quad == half) {
       cl = passbuf[q];
       ch = passbuf[4 + q];
