@@ -42,6 +42,11 @@
  *     calling thread.  A writer owns its streams, staging, device and error
  *     text, so consecutive calls on one writer may come from different
  *     threads (a goroutine migrating between OS threads); one call at a time.
+ *   - A thread waiting for a one-shot post (glfsx_post, glfsx_create of a
+ *     small blob, a Writer's tail) either polls or, past half the host's
+ *     threads, sleeps between polls; a thread that has slept once has its
+ *     timer slack set to 1 us (prctl PR_SET_TIMERSLACK) for the rest of its
+ *     life.
  *   - glfsx_last_error() is thread-local: read it in the same C call that
  *     failed (a cgo binding does so in its C preamble), or use
  *     glfsx_writer_error() for writer calls.
