@@ -125,3 +125,23 @@ def test_writer_panics_mirror_reference():
         bigblob.Machine(100).new_writer(bigblob.MemStore(1 << 20))
     with pytest.raises(_native.Panic):
         bigblob.Machine(-1)
+
+
+def test_postbench_harness_rejects_bad_arguments():
+    """tools/libpostbench.so (bench.py's postblob_concurrency leg): built by
+    build(), loads without a GPU, and refuses a run with no entry points or
+    no threads before starting any (no GPU call)."""
+    import ctypes
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tools", "libpostbench.so")
+    if not os.path.exists(path):
+        pytest.skip("tools/libpostbench.so not built")
+    lib = ctypes.CDLL(path)
+    lib.postbench_run.restype = ctypes.c_int
+    lib.postbench_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_uint64,
+                                                           ctypes.c_int, ctypes.c_char_p,
+                                                           ctypes.c_int, ctypes.c_void_p]
+    out = (ctypes.c_double * 5)()
+    assert lib.postbench_run(None, None, None, 4, 4096, 10, bytes(32), 0, out) == -1
+    assert lib.postbench_run(1, 1, 1, 0, 4096, 10, bytes(32), 0, out) == -1
+    assert lib.postbench_run(1, 1, 1, 4, 4096, 0, bytes(32), 0, out) == -1
