@@ -1831,7 +1831,7 @@ __device__ unsigned long long g_one_t[16];
 template <int QUADS>
 __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
 #if GLFSX_ONE_TIMING
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
 #endif
   __shared__ uint4 img_u4[QUADS * 64];       // the message, then its ctext
   __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
@@ -1881,8 +1881,14 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
   one_signal(dp);
   ONE_T(5);
 #if GLFSX_ONE_TIMING
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // shader clock over the kernel: [13] / [14]
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), t1 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_add(&g_one_t[13], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&g_one_t[14], (unsigned long long)(t1 - t0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(&g_one_t[15], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #endif
 }
 

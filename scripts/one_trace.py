@@ -46,6 +46,7 @@ def run(size, calls=400):
             ("read_desc", "stage", "dek", "keystream", "cid_ref", "signal"),
             (round(tv[i] / k / 100.0, 2) for i in range(6))))   # 100 MHz ticks
         out["timed_launches"] = tv[15]
+        out["k_one_clock_GHz"] = round(tv[13] / max(tv[14], 1) * 0.1, 3)
     print(json.dumps(out))
 
 
