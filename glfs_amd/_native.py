@@ -90,6 +90,7 @@ SIGNATURES = {
     "glfsx_writer_read_fd": (_INT, [_VP, _INT, _U64, _U64, ctypes.POINTER(ctypes.c_uint64)]),
     "glfsx_writer_write_device": (_INT, [_VP, _VP, _SZ, _VP]),
     "glfsx_writer_write_ctext": (_INT, [_VP, _VP, _U64, _U64, _VP]),
+    "glfsx_writer_write_ctext_blocks": (_INT, [_VP, _VP, _U64, _U64, _U64, _VP]),
     "glfsx_writer_set_strict": (_INT, [_VP, _INT]),
     "glfsx_writer_set_devices": (_INT, [_VP, _VP, _INT]),
     "glfsx_writer_error": (_CP, [_VP]),

@@ -165,6 +165,16 @@ class Writer:
             self._raise(rc)
         return n
 
+    def write_ctext_blocks(self, addrs, total: int, refs: bytes, block_size: int) -> int:
+        """write_ctext with ciphertext block j at address addrs[j] (memory
+        the caller keeps alive for the call, e.g. a NativeStore's blobs)."""
+        arr = (ctypes.c_void_p * max(len(addrs), 1))(*addrs)
+        rc = N.lib.glfsx_writer_write_ctext_blocks(self._w, arr, len(addrs), total, block_size,
+                                                   bytes(refs))
+        if rc:
+            self._raise(rc)
+        return total
+
     def flush(self) -> None:
         """Deliver the Posts of every complete block written so far."""
         rc = N.lib.glfsx_writer_flush(self._w)
@@ -488,8 +498,21 @@ def _concat(machine: "Machine", store, block_size: int, salt, roots, cid_key=Non
             if r.block_size % 64:
                 w.write(read_all(store, r))
                 continue
+            refs = b"".join(x.marshal_binary() for x in data_refs)
+            if hasattr(store, "addr"):   # blocks straight from the store's memory
+                addrs, got = [], 0
+                for i, x in enumerate(data_refs):
+                    a, n = store.addr(x.cid)
+                    want = r.block_size if i + 1 < len(data_refs) else \
+                        r.size - r.block_size * (len(data_refs) - 1)
+                    if n != want:
+                        raise ValueError(f"block {i} has {n} bytes, the root says {want}")
+                    addrs.append(a)
+                    got += n
+                w.write_ctext_blocks(addrs, got, refs, r.block_size)
+                continue
             ct = _gather(store, data_refs, r.size)
-            w.write_ctext(ct, b"".join(x.marshal_binary() for x in data_refs), r.block_size)
+            w.write_ctext(ct, refs, r.block_size)
         return w.finish()
     finally:
         w.close()
@@ -601,6 +624,14 @@ class NativeStore:
         if N.lib.glfsx_store_get(self._s, bytes(cid), ctypes.byref(p), ctypes.byref(n)):
             raise ErrNotFound(bytes(cid))
         return ctypes.string_at(p, n.value) if n.value else b""
+
+    def addr(self, cid: bytes):
+        """(address, length) of the blob in the store's own memory, valid
+        until the store is freed (glfsx_store_get)."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        if N.lib.glfsx_store_get(self._s, bytes(cid), ctypes.byref(p), ctypes.byref(n)):
+            raise ErrNotFound(bytes(cid))
+        return p.value or 0, n.value
 
     def get_into(self, cid: bytes, dst_addr: int, cap: int) -> int:
         """Copy the blob straight from the store's memory to dst_addr (at

@@ -945,7 +945,8 @@ struct glfsx_writer {
   // device input (write_device / write_ctext): events ordering the caller's
   // stream with the upload stream, and write_ctext's staging / temporaries
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  PinBuf h_ctx;
+  PinBuf h_ctx[2];            // two slabs: one gathered while the other uploads
+  hipEvent_t ev_ctx[2] = {nullptr, nullptr};
   DevBuf d_ctx, d_ptx, d_rfx;
   std::vector<WLane> lanes;  // lane 0 = the home device and streams by default
   std::vector<WSlot> slot;   // a ring: slot i runs on lane i % lanes.size()
@@ -1023,7 +1024,16 @@ struct CopyTask {
   void *rctx = nullptr;
   uint64_t off = 0;
   int64_t *got = nullptr;
+  // blocks != nullptr: gather nblk blocks (bsz bytes each, the last lastn)
+  // into dst back to back instead (par_gather)
+  const void *const *blocks = nullptr;
+  uint64_t nblk = 0, bsz = 0, lastn = 0;
 };
+void gather_blocks(uint8_t *dst, const void *const *blocks, uint64_t k, uint64_t bs,
+                   uint64_t last) {
+  for (uint64_t i = 0; i < k; ++i)
+    memcpy(dst + i * bs, blocks[i], i + 1 == k ? last : bs);
+}
 
 // Read n bytes at offset off through fn, repeating short reads; stops early
 // only at the end of the input (fn returns 0) or on an error (< 0).
@@ -1051,7 +1061,9 @@ struct CopyPool {
         t = q.back();
         q.pop_back();
       }
-      if (t.read_at)
+      if (t.blocks)
+        gather_blocks(t.dst, t.blocks, t.nblk, t.bsz, t.lastn);
+      else if (t.read_at)
         *t.got = read_full(t.read_at, t.rctx, t.dst, t.n, t.off);
       else
         memcpy(t.dst, t.src, t.n);
@@ -1172,6 +1184,49 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n, int dev = -1) {
   }
   P.cv.notify_all();
   memcpy(dst, src, std::min(per, n));
+  while (left.load(std::memory_order_acquire) > 0) sched_yield();
+}
+
+// k blocks (bs bytes each, the last `last`) from scattered addresses into
+// dst back to back, over the copy pool (Concat's ctext straight from the
+// store's memory into the Writer's pinned staging).  Blocks of >= 4 MiB go
+// one par_memcpy each; smaller ones in runs of consecutive blocks per thread.
+void par_gather(uint8_t *dst, const void *const *blocks, uint64_t k, uint64_t bs,
+                uint64_t last, int dev = -1) {
+  if (k == 0) return;
+  if (bs >= (4ull << 20)) {
+    for (uint64_t i = 0; i < k; ++i)
+      par_memcpy(dst + i * bs, static_cast<const uint8_t *>(blocks[i]), i + 1 == k ? last : bs,
+                 dev);
+    return;
+  }
+  const uint64_t total = (k - 1) * bs + last;
+  CopyPool &P = copy_pool(dev);
+  const uint64_t parts =
+      std::min<uint64_t>({uint64_t(P.workers) + 1, k, std::max<uint64_t>(1, total >> 18)});
+  if (parts <= 1) {
+    gather_blocks(dst, blocks, k, bs, last);
+    return;
+  }
+  const uint64_t per = (k + parts - 1) / parts;
+  std::atomic<int> left{0};
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (uint64_t b = per; b < k; b += per) {
+      const uint64_t m = std::min(per, k - b);
+      CopyTask t{};
+      t.dst = dst + b * bs;
+      t.left = &left;
+      t.blocks = blocks + b;
+      t.nblk = m;
+      t.bsz = bs;
+      t.lastn = b + m == k ? last : bs;
+      left.fetch_add(1, std::memory_order_relaxed);
+      P.q.push_back(t);
+    }
+  }
+  P.cv.notify_all();
+  gather_blocks(dst, blocks, std::min(per, k), bs, per >= k ? last : bs);
   while (left.load(std::memory_order_acquire) > 0) sched_yield();
 }
 
@@ -2135,39 +2190,53 @@ int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
   return 0;
 }
 
-int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
-                             uint64_t block_size, const uint8_t *refs) {
+int glfsx_writer_write_ctext_blocks(glfsx_writer *w, const void *const *blocks,
+                                    uint64_t nblocks, uint64_t total, uint64_t block_size,
+                                    const uint8_t *refs) {
   if (!w) return fail(GLFSX_E_ARG, "null writer");
   WriterCall call(w);
   if (w->sticky) return call.done(fail(w->sticky, "%s", w->err.c_str()));
   if (total == 0) return 0;
-  if (!ctext || !refs) return call.done(fail(GLFSX_E_ARG, "null argument"));
+  if (!blocks || !refs) return call.done(fail(GLFSX_E_ARG, "null argument"));
   if (w->lanes.size() != 1)
     return call.done(fail(GLFSX_E_UNSUPPORTED, "device input needs a one-device writer"));
   if (block_size == 0 || block_size % 64)
     return call.done(fail(GLFSX_E_UNSUPPORTED, "decrypt needs block_size %% 64 == 0"));
+  const uint64_t nb = (total + block_size - 1) / block_size;
+  if (nblocks != nb)
+    return call.done(fail(GLFSX_E_ARG, "%llu blocks given, %llu bytes need %llu",
+                          (unsigned long long)nblocks, (unsigned long long)total,
+                          (unsigned long long)nb));
   auto go = [&]() -> int {
     if (!w->ev_in) {
       HIP_TRY(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
     }
-    const uint64_t nb = (total + block_size - 1) / block_size;
+    for (hipEvent_t &ev : w->ev_ctx)
+      if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const uint64_t slab = std::max<uint64_t>(1, (64ull << 20) / block_size);
-    if (int e = w->h_ctx.ensure(slab * block_size + 64 * slab)) return e;
+    for (PinBuf &hb : w->h_ctx)
+      if (int e = hb.ensure(slab * block_size + 64 * slab)) return e;
     if (int e = w->d_ctx.ensure(slab * block_size + 64)) return e;
     if (int e = w->d_ptx.ensure(slab * block_size + 64)) return e;
     if (int e = w->d_rfx.ensure(64 * slab)) return e;
-    for (uint64_t b0 = 0; b0 < nb; b0 += slab) {
+    // slab i is gathered into host buffer i & 1 while slab i - 1 uploads,
+    // decrypts and goes into the Writer (all on s_up, in order: the device
+    // temporaries are reused in stream order); buffer i & 1 is free once
+    // slab i - 2's uploads are done
+    const int dev = w->lanes[0].dev;
+    uint64_t i = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += slab, ++i) {
       const uint64_t k = std::min(slab, nb - b0);
       const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
-      // the staging and temporaries are reused: the previous slab's
-      // upload, decrypt and copy-out (all on s_up) must be done
-      HIP_TRY(hipStreamSynchronize(w->s_up));
-      par_memcpy(w->h_ctx.u8(), static_cast<const uint8_t *>(ctext) + b0 * block_size, bytes);
-      memcpy(w->h_ctx.u8() + bytes, refs + 64 * b0, 64 * k);
-      HIP_TRY(hipMemcpyAsync(w->d_ctx.p, w->h_ctx.p, bytes, hipMemcpyHostToDevice, w->s_up));
-      HIP_TRY(hipMemcpyAsync(w->d_rfx.p, w->h_ctx.u8() + bytes, 64 * k,
-                             hipMemcpyHostToDevice, w->s_up));
+      PinBuf &hb = w->h_ctx[i & 1];
+      if (i >= 2) HIP_TRY(hipEventSynchronize(w->ev_ctx[i & 1]));
+      par_gather(hb.u8(), blocks + b0, k, block_size, bytes - (k - 1) * block_size, dev);
+      memcpy(hb.u8() + bytes, refs + 64 * b0, 64 * k);
+      HIP_TRY(hipMemcpyAsync(w->d_ctx.p, hb.p, bytes, hipMemcpyHostToDevice, w->s_up));
+      HIP_TRY(hipMemcpyAsync(w->d_rfx.p, hb.u8() + bytes, 64 * k, hipMemcpyHostToDevice,
+                             w->s_up));
+      HIP_TRY(hipEventRecord(w->ev_ctx[i & 1], w->s_up));
       HIP_TRY(launch_decrypt(w->d_ctx.u8(), w->d_ptx.u8(), k, block_size,
                              bytes - (k - 1) * block_size, w->d_rfx.u8(), w->s_up));
       if (int e = write_dev(w, w->d_ptx.u8(), bytes)) return e;
@@ -2179,6 +2248,22 @@ int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
   };
   if (int e = go()) return call.done(w->sticky = e);
   return 0;
+}
+
+int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
+                             uint64_t block_size, const uint8_t *refs) {
+  if (!w) return fail(GLFSX_E_ARG, "null writer");
+  if (total == 0 || !ctext || block_size == 0 || block_size % 64) {
+    // (the same checks and errors; nothing to split into blocks)
+    const void *one = ctext;
+    return glfsx_writer_write_ctext_blocks(w, ctext ? &one : nullptr, 0, total, block_size,
+                                           refs);
+  }
+  const uint64_t nb = (total + block_size - 1) / block_size;
+  std::vector<const void *> blocks(nb);
+  for (uint64_t j = 0; j < nb; ++j)
+    blocks[j] = static_cast<const uint8_t *>(ctext) + j * block_size;
+  return glfsx_writer_write_ctext_blocks(w, blocks.data(), nb, total, block_size, refs);
 }
 
 int glfsx_writer_set_strict(glfsx_writer *w, int strict) {
@@ -2255,9 +2340,10 @@ void glfsx_writer_free(glfsx_writer *w) {
       release_stream_scratch(st);
       (void)hipStreamDestroy(st);
     }
-  for (hipEvent_t ev : {w->ev_in, w->ev_out})
+  for (hipEvent_t ev : {w->ev_in, w->ev_out, w->ev_ctx[0], w->ev_ctx[1]})
     if (ev) (void)hipEventDestroy(ev);
-  if (w->h_ctx.p) (void)hipHostFree(w->h_ctx.p);
+  for (PinBuf &b : w->h_ctx)
+    if (b.p) (void)hipHostFree(b.p);
   for (void *p : {w->d_ctx.p, w->d_ptx.p, w->d_rfx.p})
     if (p) (void)hipFree(p);
   delete w;

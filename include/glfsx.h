@@ -210,6 +210,14 @@ int glfsx_writer_write_device(glfsx_writer *w, const void *d_data, size_t n,
  * side fused with its Writer. */
 int glfsx_writer_write_ctext(glfsx_writer *w, const void *ctext, uint64_t total,
                              uint64_t block_size, const uint8_t *refs);
+/* The same with the ciphertext blocks at scattered addresses (nblocks =
+ * ceil(total / block_size); block j at blocks[j], block_size bytes, the last
+ * one short): Concat straight from a store's memory, each 64 MiB slab of
+ * blocks gathered into pinned staging by the copy threads while the previous
+ * one uploads and decrypts. */
+int glfsx_writer_write_ctext_blocks(glfsx_writer *w, const void *const *blocks,
+                                    uint64_t nblocks, uint64_t total, uint64_t block_size,
+                                    const uint8_t *refs);
 /* A Writer's io.ReaderFrom (no reference counterpart; io.Copy in Create and
  * Concat, blob.go:213,341, uses it when the Writer has it): reserve lends
  * the caller the next *cap >= 1 bytes of the writer's pinned staging at

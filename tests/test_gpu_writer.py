@@ -234,6 +234,27 @@ def test_concat_write_ctext_vs_oracle(gpu, O):
     assert bigblob.read_all(st, got) == b"".join(parts)
 
 
+def test_concat_from_store_memory_many_slabs(gpu, O):
+    """Concat from a NativeStore takes each ciphertext block straight from
+    the store's memory (glfsx_writer_write_ctext_blocks: 64 MiB slabs of
+    scattered blocks gathered into two pinned buffers in turn): 200 MiB
+    (four slabs, so both buffers are reused) plus a ragged second root ==
+    the oracle's Create of the joined bytes, and == the contiguous route
+    (a MemStore: gathered in Python, glfsx_writer_write_ctext)."""
+    from glfs_amd import bigblob
+    bs = 1 << 20
+    m = bigblob.Machine(bs)
+    parts = [O.fill_splitmix(200 * bs + 12345, 91), O.fill_splitmix(3 * bs + 7, 92)]
+    st = bigblob.NativeStore(bs, "trust")
+    roots = [m.create(st, None, p) for p in parts]
+    got = m.concat(st, bs, None, *roots)
+    want = O.create(b"".join(parts), bs)[0]
+    assert got.ref.marshal_binary() == want
+    ms = bigblob.MemStore(bs)
+    roots2 = [m.create(ms, None, p) for p in parts]
+    assert m.concat(ms, bs, None, *roots2).ref.marshal_binary() == want
+
+
 class _ChunkyReader:
     """An io.Reader whose Reads return random amounts (1 B .. 3 MiB), read
     into the caller's buffer (readinto), like a pipe or socket."""
