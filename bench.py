@@ -177,12 +177,14 @@ def main():
     barrier()
     torch.cuda.synchronize()
     N.check(N.lib.glfsx_clock_probe(1, None))   # (synchronous; before the clock starts)
+    reruns0 = N.lib.glfsx_fused_failures()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    reruns = {"headline": N.lib.glfsx_fused_failures() - reruns0}
     probe = (ctypes.c_uint64 * 2)()
     N.check(N.lib.glfsx_clock_probe(0, probe))
     step_clock = round(probe[0] / probe[1] * 0.1, 3) if probe[1] else None
@@ -261,17 +263,29 @@ def main():
             if world == 1:   # the CPU baseline is an N=1 figure (rank 0 only)
                 out["cpu_baseline"] = cpu_baseline(args)
             if args.host_rt_gib > 0:
+                r0 = N.lib.glfsx_fused_failures()
                 out["config2"] = config2_leg(torch, N, stream, sp)
+                reruns["config2"] = N.lib.glfsx_fused_failures() - r0
                 out["small_blobs"] = small_blobs(torch, N, stream, sp)
                 out["small_blobs_from_host"] = small_blobs_from_host(torch, N, stream, sp)
+                r0 = N.lib.glfsx_fused_failures()
                 out["config4_end_to_end"] = config4_end_to_end(torch, N, stream, sp)
+                reruns["config4"] = N.lib.glfsx_fused_failures() - r0
                 if world == 1 and "cpu_baseline" in out:
                     out["cpu_baseline"].update(
                         cpu_baseline_configs(args, out["config2"]["root_cid"]))
+    # a one-launch split post that failed was discarded and re-run with two
+    # launches inside the timed region: the line says how often (0 expected),
+    # and a non-zero count fails the run (glfsx_fused_failures)
+    out["fused_reruns"] = reruns
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if any(reruns.values()):
+        print(f"bench.py: one-launch split posts were re-run: {reruns}", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
 
 
 def gpu_numa_node(torch, dev):
@@ -362,10 +376,12 @@ def main_one_process(args, devs, host_node=None):
     for _ in range(args.warmup):
         step()
     sync_all()
+    reruns0 = N.lib.glfsx_fused_failures()
     t0 = time.perf_counter()
     parts = [step() for _ in range(args.steps)]
     sync_all()
     dt = time.perf_counter() - t0
+    reruns = {"headline": N.lib.glfsx_fused_failures() - reruns0}
     ms = dt / args.steps * 1e3
     mean = [sum(p[k] for p in parts) / len(parts) for k in range(len(parts[0]))] if parts else []
     out = {
@@ -407,7 +423,12 @@ def main_one_process(args, devs, host_node=None):
         del bufs, cts
         if args.host_rt_gib > 0:
             out["host_round_trip"] = multi_lane_host(torch, N, args, devs, bs)
+    out["fused_reruns"] = reruns
     print(json.dumps(out), flush=True)
+    if any(reruns.values()):
+        print(f"bench.py: one-launch split posts were re-run: {reruns}", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
 
 
 def multi_lane_host(torch, N, args, devs, bs):
@@ -638,6 +659,21 @@ def roofline(torch, N, data, ctext, per, bs, stream, sp, reps=5, step_ms=None, t
     return roof, valu
 
 
+def job_cores():
+    """Threads the CPU baselines run: the job's core share (OMP_NUM_THREADS,
+    16 on the GPU box), at most the CPUs this process may run on."""
+    aff = len(os.sched_getaffinity(0))
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff, aff))
+
+
+def core_info():
+    """What the job_cores figures ran on: the thread
+    count used, the affinity mask's size, OMP_NUM_THREADS and the host's
+    whole CPU count (nproc) -- the job is a share of the host, not all of it."""
+    return {"job_cores": job_cores(), "sched_affinity": len(os.sched_getaffinity(0)),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "nproc": os.cpu_count()}
+
+
 def cpu_baseline(args):
     """The reference's per-block sequence (ref.go:98-161: keyed BLAKE3 DEK,
     ChaCha20 XOR, BLAKE3 CID of the ctext, ctext into a buffer) timed on host
@@ -648,11 +684,10 @@ def cpu_baseline(args):
     with a portable scalar ChaCha20 (as x/crypto's generic Go ChaCha20, the
     one amd64 runs, go.mod:10) -- oracle_post_batch_gomix.  Beside it: the
     all-scalar oracle port, the all-SIMD libraries (OpenSSL ChaCha20), and
-    the Go mix on all cores of this job over independent block ranges."""
+    the Go mix on the job's cores (job_cores) over independent block ranges."""
     from oracle import oracle as O
     L = O.lib()
-    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(),
-                       os.cpu_count()))
+    cores = job_cores()
     n = args.cpu_sample_mib * MIB
     n_all = 4 * n
     buf = ctypes.create_string_buffer(n_all)
@@ -691,18 +726,18 @@ def cpu_baseline(args):
             "sample": f"{args.cpu_sample_mib} MiB = {n // args.block_size} x "
                       f"{args.block_size // 1024} KiB blocks, oracle_post_batch_gomix, "
                       f"1 thread, {dgo1:.1f} s",
-            "all_cores": {"value": r4(goall), "cores": cores,
+            "job_cores": {"value": r4(goall), "cores": cores,
                           "sample": f"{4 * args.cpu_sample_mib} MiB, {cores} threads over "
                                     f"independent block ranges, {dgoall:.1f} s"},
             "scalar_port": {"value": r4(port1), "cores": 1,
                             "sample": f"{port_n // MIB} MiB, oracle_post_batch (portable "
                                       f"scalar BLAKE3 and ChaCha20), {dport1:.1f} s"},
             "simd_libraries": {"value": r4(simd1), "cores": 1,
-                               "all_cores": {"value": r4(simdall), "cores": cores},
+                               "job_cores": {"value": r4(simdall), "cores": cores},
                                "sample": f"upstream BLAKE3 C (AVX-512) + OpenSSL ChaCha20 "
                                          f"(AVX-512), {dsimd1:.1f} s / {dsimdall:.1f} s",
                                "what": "an upper bound for any per-core CPU path"},
-            "nproc": os.cpu_count(), "cpu_model": model}
+            "host_cores": core_info(), "cpu_model": model}
 
 
 def small_blobs(torch, N, stream, sp, n=1 << 20, ln=4096, reps=10):
@@ -814,8 +849,7 @@ def cpu_baseline_configs(args, config2_root_cid):
     import hashlib
     from oracle import oracle as O
     L = O.lib()
-    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(),
-                       os.cpu_count()))
+    cores = job_cores()
     tsalt = O.derive_key(bytes(32), b"blob")            # machine.go:50-54
     raw, idx = O.derive_key(tsalt, b"raw"), O.derive_key(tsalt, b"index")
     out = {}
@@ -827,7 +861,7 @@ def cpu_baseline_configs(args, config2_root_cid):
     nb = size // bs
     refs = ctypes.create_string_buffer(64 * nb)
     c2 = {}
-    for label, th in (("one_core", 1), ("all_cores", cores)):
+    for label, th in (("one_core", 1), ("job_cores", cores)):
         t = time.perf_counter()
         rc = L.oracle_post_batch_gomix(refs, ct, raw, buf, size, bs, None, th)
         root_ref, _ = O.post(idx, refs.raw.ljust(bs, b"\0"))   # the one index node
@@ -849,7 +883,7 @@ def cpu_baseline_configs(args, config2_root_cid):
     refs = ctypes.create_string_buffer(64 * n)
     want = _GPU_REFS.get("small_blobs_seed0")
     sb = {}
-    for label, th, m in (("one_core", 1, n // 4), ("all_cores", cores, n)):
+    for label, th, m in (("one_core", 1, n // 4), ("job_cores", cores, n)):
         t = time.perf_counter()
         rc = L.oracle_post_batch_gomix(refs, ct, raw, buf, m * ln, ln, None, th)
         dt = time.perf_counter() - t
@@ -863,7 +897,7 @@ def cpu_baseline_configs(args, config2_root_cid):
                                          hashlib.sha256(got).digest() ==
                                          hashlib.sha256(want[:64 * m]).digest())}
     sb.update({"unit": "GiB/s", "kind": "port",
-               "sample": "one_core: the first 262,144 of the 1,048,576 blobs; all_cores: all"})
+               "sample": "one_core: the first 262,144 of the 1,048,576 blobs; job_cores: all"})
     out["small_blobs"] = sb
     return out
 

@@ -69,6 +69,8 @@ SIGNATURES = {
     "glfsx_set_split_target": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_set_latency_wgs": (ctypes.c_uint32, [ctypes.c_uint32]),
     "glfsx_debug_fused": (_U64, [ctypes.c_uint32, _U64]),
+    "glfsx_fused_failures": (_U64, []),
+    "glfsx_debug_one_drop": (None, [ctypes.c_uint32]),
     "glfsx_clock_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     "glfsx_one_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     "glfsx_derive_key": (_INT, [_VP, _SZ, _CP, _VP, _SZ]),

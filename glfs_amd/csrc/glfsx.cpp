@@ -270,7 +270,8 @@ struct OneLane {
   uint32_t seq = 0;           // the last launch's sequence number
   OneDesc *h_desc = nullptr;  // pinned, kOneBatch descriptors
   OneDesc *d_desc = nullptr;  // the kernel's view of h_desc
-  uint32_t *h_flag = nullptr, *d_flag = nullptr;  // pinned, kOneBatch flags
+  // pinned, kOneBatch flags + one nobody waits on (glfsx_debug_one_drop)
+  uint32_t *h_flag = nullptr, *d_flag = nullptr;
   // medium posts: device copies of the messages, and per descriptor
   // kMedAuxWords words of CVs / arrival counter / DEK (zeroed when grown;
   // the kernels leave every counter at zero)
@@ -307,7 +308,7 @@ int poster_get(int dev, OnePoster **out) {
         hipEventCreateWithFlags(&l.ev, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&h, sizeof(OneDesc) * kOneBatch, hipHostMallocDefault) != hipSuccess ||
         hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
-        hipHostMalloc(&hf, sizeof(uint32_t) * kOneBatch, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc(&hf, sizeof(uint32_t) * (kOneBatch + 1), hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(&df, hf, 0) != hipSuccess) {
       for (OneLane &x : p->lane) {
         if (x.h_desc) (void)hipHostFree(x.h_desc);
@@ -324,7 +325,7 @@ int poster_get(int dev, OnePoster **out) {
     l.d_desc = static_cast<OneDesc *>(d);
     l.h_flag = static_cast<uint32_t *>(hf);
     l.d_flag = static_cast<uint32_t *>(df);
-    memset(hf, 0, sizeof(uint32_t) * kOneBatch);
+    memset(hf, 0, sizeof(uint32_t) * (kOneBatch + 1));
   }
   g_posters[dev].store(p, std::memory_order_release);
   *out = p;
@@ -339,10 +340,17 @@ void pending_push(OnePoster *P, OneReq *r) {
                                              std::memory_order_relaxed));
 }
 
+// Test hook (glfsx_debug_one_drop): the next launch sends request k's
+// result flag to the lane's spare word, as a launch that failed on the
+// device would leave it: the request's caller must see the error, and no
+// caller may return while a request of its call is still queued.
+std::atomic<uint32_t> g_one_drop{~0u};
+
 // One launch of k_one over the batch's small messages and one launch_med
 // (two kernels) over its medium ones, on the lane's stream; request i's
 // flag is lane.h_flag[i], set to `seq` when its results are in place.
 int one_launch(OneLane &L, const std::vector<OneReq *> &batch, uint32_t seq) {
+  const uint32_t drop = g_one_drop.exchange(~0u, std::memory_order_relaxed);
   uint64_t max_small = 0, max_med = 0, med_bytes = 0;
   size_t ns = 0, nm = 0;
   for (const OneReq *r : batch) {
@@ -368,7 +376,7 @@ int one_launch(OneLane &L, const std::vector<OneReq *> &batch, uint32_t seq) {
   for (size_t k = 0; k < batch.size(); ++k) {
     const OneReq *r = batch[k];
     OneDesc d = r->d;
-    d.flag = L.d_flag + k;
+    d.flag = L.d_flag + (k == drop ? kOneBatch : k);
     d.seq = seq;
     if (r->d.len <= kMaxOneLen) {
       L.h_desc[is++] = d;
@@ -401,14 +409,25 @@ const int kOneSpinners = [] {
 }();
 constexpr int64_t kOneSpinNs = 300000;
 // A sleeping waiter's 10 us sleeps would otherwise end up to the default
-// 50 us timer slack late: once per thread, its slack is set to 1 us.
-void one_sleep_slack() {
-  static thread_local bool set = [] {
+// 50 us timer slack late: while a caller's thread sleeps in a one-shot wait
+// its slack is 1 us, and the thread's own slack is restored when the wait
+// returns (the caller's thread -- a Go runtime M, an application thread --
+// is not the library's to retune).
+struct SleepSlack {
+  long saved = -1;
+  void on() {
+    if (saved >= 0) return;
+    saved = prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL);
+    if (saved < 0) {
+      saved = -2;  // unknown: leave it alone
+      return;
+    }
     prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
-    return true;
-  }();
-  (void)set;
-}
+  }
+  ~SleepSlack() {
+    if (saved >= 0) prctl(PR_SET_TIMERSLACK, static_cast<unsigned long>(saved), 0UL, 0UL, 0UL);
+  }
+};
 
 // Post rs[0..n) on device dev (the calling thread's current device); returns
 // when every request's ctext and ref are in its staging.
@@ -434,14 +453,27 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
       if (spin) P->spinners.fetch_sub(1, std::memory_order_relaxed);
     }
   } unspin{P, spin};
+  SleepSlack slack;
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t sleeps = 0;
-  size_t ndone = 0;  // rs[0..ndone) are finished or failed
+  // Once a launch of ours is seen to have failed on the device (frc), the
+  // call still returns only when no request of it can be touched again: each
+  // is failed before launch, finished, or armed on a lane whose launch has
+  // completed.  A request still on the pending stack would otherwise be
+  // launched -- its descriptor read, its flag and staging written -- after
+  // its caller freed it.
+  int frc = 0;
+  std::string ferr;
+  auto settled = [&frc](const OneReq *r) {
+    if (r->done.load(std::memory_order_acquire) || one_finished(r)) return true;
+    return frc && r->armed.load(std::memory_order_acquire) &&
+           hipEventQuery(r->lane->ev) != hipErrorNotReady;
+  };
+  size_t ndone = 0;  // rs[0..ndone) are settled
   for (uint32_t spins = 0;; ++spins) {
-    while (ndone < n && (rs[ndone]->done.load(std::memory_order_acquire) ||
-                         one_finished(rs[ndone])))
-      ++ndone;
+    while (ndone < n && settled(rs[ndone])) ++ndone;
     if (ndone == n) {
+      if (frc) return fail(frc, "%s", ferr.c_str());
       for (size_t i = 0; i < n; ++i)
         if (rs[i]->rc) return fail(rs[i]->rc, "%s", rs[i]->err.c_str());
       return 0;
@@ -531,9 +563,9 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
     }
     // sleepers back off 10 -> 40 us: hundreds of them must not wake 100 k
     // times a second each
-    one_sleep_slack();
+    slack.on();
     std::this_thread::sleep_for(std::chrono::microseconds(10u << std::min(sleeps, 2u)));
-    if (++sleeps % 1024 == 0) {
+    if (!frc && ++sleeps % 1024 == 0) {
       // a long wait: a launch that failed on the device never sets its flags
       for (size_t i = ndone; i < n; ++i) {
         const OneReq *r = rs[i];
@@ -542,9 +574,11 @@ int one_post_many(int dev, OneReq *const *rs, size_t n) {
         // has completed when it has)
         const hipError_t q = hipEventQuery(r->lane->ev);
         if (q == hipErrorNotReady || one_finished(r)) continue;
-        return fail(GLFSX_E_DEVICE, "one-shot post: %s",
-                    q == hipSuccess ? "the launch completed without its result flag"
-                                    : hipGetErrorString(q));
+        frc = GLFSX_E_DEVICE;
+        ferr = std::string("one-shot post: ") +
+               (q == hipSuccess ? "the launch completed without its result flag"
+                                : hipGetErrorString(q));
+        break;
       }
     }
   }
@@ -1573,6 +1607,10 @@ uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us) {
   fused_debug(skip_msg, wait_us);
   return fused_timeouts();
 }
+
+uint64_t glfsx_fused_failures(void) { return fused_timeouts(); }
+
+void glfsx_debug_one_drop(uint32_t k) { g_one_drop.store(k, std::memory_order_relaxed); }
 
 int glfsx_one_stats(int reset, uint64_t out[3]) {
   for (int i = 0; i < 3; ++i) {

@@ -49,9 +49,6 @@ uint32_t fused_errors_take(hipStream_t s);
 void fused_debug(uint32_t skip_msg, uint64_t wait_us);
 // Timeouts seen by fused_errors_take so far (process-wide).
 uint64_t fused_timeouts();
-// The same hooks for the one-call tree route's tree items: takes the pending
-// skip (a tree block whose DEK is computed but never flagged ready; ~0u:
-// none) and the wait bound; a timeout the host saw is counted.
 // The bulk passes' clock probe on the current device (k_pass): out[0] =
 // shader-clock cycles, out[1] = 100 MHz ticks summed over every k_pass
 // workgroup since the last reset; reset: zero them after reading.
@@ -102,7 +99,6 @@ struct SmallJob {
 // The small route's limit for blobs of block size bs.
 inline uint64_t small_max_for(uint64_t bs) { return bs < kMaxSmallLen ? bs : kMaxSmallLen; }
 hipError_t launch_post_small(const SmallJob &job, hipStream_t s);
-// The tree items of d_tree (device memory, 2 x spans items) in one launch.
 
 // One-shot posts (ref.go:98-161 for one message of at most kMaxOneLen bytes:
 // a glfs.PostBlob of a small blob, a Writer's tail block, an index node of a

@@ -432,6 +432,9 @@ struct KArgs {
   uint32_t split_log2;
   uint32_t *scratch;
   uint32_t *cnt;
+  // the clock probe's two counters on this launch's device (g_clk), or
+  // nullptr: probing is off until the process first calls clock_probe
+  unsigned long long *clk;
 };
 
 // Split mode: thread 0 publishes this workgroup's subtree CV and counts it
@@ -1218,12 +1221,14 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   WGT(bid, 3);
 }
 
-// Clock probe of the bulk passes (glfsx_clock_probe): every k_pass
-// workgroup adds its lifetime in shader-clock cycles (s_memtime) and in
-// 100 MHz ticks (s_memrealtime) to these two device words, so a caller reads
-// the clock the chip held over exactly the launches it timed:
-// cycles / ticks x 100 MHz.  Two scalar timer reads per wave and two atomic
-// adds per workgroup (thread 0).
+// Clock probe of the bulk passes (glfsx_clock_probe): once a process has
+// called it, every k_pass workgroup adds its lifetime in shader-clock cycles
+// (s_memtime) and in 100 MHz ticks (s_memrealtime) to these two device
+// words (KArgs::clk), so a caller reads the clock the chip held over the
+// launches since its reset: cycles / ticks x 100 MHz.  Two scalar timer
+// reads per wave and, when on, two atomic adds per workgroup (thread 0).
+// The words are per device, not per launch: k_pass launches of other
+// callers on the same device in that window are counted too.
 __device__ unsigned long long g_clk[2];
 
 template <int G, bool CHACHA, bool ALIGNED, int A = 2>
@@ -1231,11 +1236,11 @@ __global__ __launch_bounds__(256) void k_pass(KArgs a) {
   __shared__ uint4 lds_u4[512 + kStageOf<CHACHA>];
   const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   pass_body<G, CHACHA, ALIGNED, A, 0>(a, blockIdx.x, lds_u4, nullptr);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && a.clk) {
     const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    __hip_atomic_fetch_add(&g_clk[0], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(&a.clk[0], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(&g_clk[1], (unsigned long long)(r1 - r0), __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(&a.clk[1], (unsigned long long)(r1 - r0), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -2873,8 +2878,26 @@ hipError_t launch_small_pass(const SArgs &a, uint64_t max_len, hipStream_t s) {
   }
 }
 
+// The clock probe (g_clk): off until clock_probe is first called.
+std::atomic<bool> g_clk_on{false};
+std::atomic<unsigned long long *> g_clk_addr[64];
+unsigned long long *clk_words() {
+  if (!g_clk_on.load(std::memory_order_relaxed)) return nullptr;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+  unsigned long long *p = g_clk_addr[d].load(std::memory_order_acquire);
+  if (!p) {
+    void *q = nullptr;
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_clk)) != hipSuccess) return nullptr;
+    p = static_cast<unsigned long long *>(q);
+    g_clk_addr[d].store(p, std::memory_order_release);
+  }
+  return p;
+}
+
 KArgs make_args(const PostJob &job) {
   KArgs a{};
+  a.clk = clk_words();
   a.src = job.src;
   a.ctext = job.ctext;
   a.stride = job.stride;
@@ -3142,6 +3165,7 @@ extern "C" int glfsx_debug_one_timing(int reset, uint64_t out[16]) {
 #endif
 
 hipError_t clock_probe(int reset, uint64_t out[2]) {
+  g_clk_on.store(true, std::memory_order_relaxed);
   unsigned long long v[2] = {0, 0};
   hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_clk), sizeof v, 0, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return e;

@@ -44,9 +44,9 @@
  *     threads (a goroutine migrating between OS threads); one call at a time.
  *   - A thread waiting for a one-shot post (glfsx_post, glfsx_create of a
  *     small blob, a Writer's tail) either polls or, past half the host's
- *     threads, sleeps between polls; a thread that has slept once has its
- *     timer slack set to 1 us (prctl PR_SET_TIMERSLACK) for the rest of its
- *     life.
+ *     threads, sleeps between polls; while it sleeps in that wait its timer
+ *     slack is 1 us (prctl PR_SET_TIMERSLACK), and the thread's own slack
+ *     is restored before the call returns.
  *   - glfsx_last_error() is thread-local: read it in the same C call that
  *     failed (a cgo binding does so in its C preamble), or use
  *     glfsx_writer_error() for writer calls.
@@ -122,6 +122,18 @@ uint32_t glfsx_set_latency_wgs(uint32_t wgs);
  * bound to wait_us microseconds (0: the default, 1 s).  Returns the number
  * of failed one-launch posts seen so far, process-wide. */
 uint64_t glfsx_debug_fused(uint32_t skip_msg, uint64_t wait_us);
+/* Measurement hook (no reference counterpart): the number of failed
+ * one-launch split posts seen so far, process-wide -- each one was discarded
+ * and re-run with two launches.  Reads a counter and nothing else (unlike
+ * glfsx_debug_fused, it leaves the skip / bound state alone); bench.py
+ * prints its delta over every timed leg as `fused_reruns`. */
+uint64_t glfsx_fused_failures(void);
+/* Test hook (no reference counterpart): the next one-shot launch (the
+ * coalesced launch behind a single-block Create / PostBlob and the few-block
+ * and medium-blob batches) withholds the result flag of its request k, as a
+ * launch that failed on the device would; the waiting call fails with
+ * GLFSX_E_DEVICE once that launch has completed.  ~0u: none. */
+void glfsx_debug_one_drop(uint32_t k);
 
 /* Measurement hook (no reference counterpart): the bulk hashing passes
  * (one workgroup per block) add each workgroup's lifetime in shader-clock

@@ -79,12 +79,14 @@ static int derive_key(uint8_t *out, size_t n, const uint8_t *salt, const void *i
 import "C"
 
 import (
+	"bytes"
 	"context"
 	"errors"
 	"fmt"
 	"io"
 	"math"
 	"os"
+	"reflect"
 	"runtime/cgo"
 	"strconv"
 	"strings"
@@ -212,15 +214,49 @@ func (gw *gpuWriter) Write(data []byte) (int, error) {
 	return len(data), nil
 }
 
-// osFile is what ReadFrom needs of a file: matched as an interface, not as
-// *os.File, because since Go 1.22 io.Copy(w, f) calls f.WriteTo, which for a
-// writer that is not a socket calls io.Copy(w, fileWithoutWriteTo{f}) -- a
-// wrapper embedding *os.File, so ReadFrom never sees the *os.File itself but
-// the wrapper has these methods (ADVICE r4).
+// osFile is what ReadFrom needs of a file.
 type osFile interface {
 	Fd() uintptr
 	Stat() (os.FileInfo, error)
 	io.Seeker
+}
+
+// plainFile returns r as a file whose Read is the file's own read(2), or
+// false: an *os.File, or io.Copy's own wrapper of one (since Go 1.22
+// io.Copy(w, f) calls f.WriteTo, which for a writer that is not a socket
+// calls io.Copy(w, fileWithoutWriteTo{f}), so ReadFrom never sees the
+// *os.File itself -- ADVICE r4).  Matched by exact dynamic type, never by
+// method set: a user type that embeds *os.File and overrides Read (to
+// transform or limit the bytes) has every osFile method too, and the pread
+// route would bypass its Read (ADVICE r5).
+func plainFile(r io.Reader) (osFile, bool) {
+	if f, ok := r.(*os.File); ok {
+		return f, true
+	}
+	if reflect.TypeOf(r).String() == "os.fileWithoutWriteTo" {
+		f, ok := r.(osFile)
+		return f, ok
+	}
+	return nil, false
+}
+
+// positionedReader returns r as an io.ReaderAt + io.Seeker whose Read is
+// ReadAt at the current offset, or false: the standard library's own types
+// only, for the same reason as plainFile (an embedding type's Read may
+// differ from the ReadAt it promotes).
+func positionedReader(r io.Reader) (interface {
+	io.ReaderAt
+	io.Seeker
+}, bool) {
+	switch x := r.(type) {
+	case *io.SectionReader:
+		return x, true
+	case *bytes.Reader:
+		return x, true
+	case *strings.Reader:
+		return x, true
+	}
+	return nil, false
 }
 
 // fdRouteReads counts ReadFrom calls served by the pread route (gpu_test.go).
@@ -231,19 +267,20 @@ func gpuDeviceCount() int { return int(C.glfsx_device_count()) }
 
 // ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341).
 //   - A regular file (an *os.File, or io.Copy's fileWithoutWriteTo wrapper
-//     of one): read from its current offset to its end by the library's
-//     reader threads with pread(2), straight into the writer's pinned
-//     staging, while earlier batches hash (glfsx_writer_read_fd); the file
-//     is left positioned after what was read, as io.Copy leaves it.
-//   - An io.ReaderAt that is also an io.Seeker (*io.SectionReader, ...): the
-//     same through ReadAt from several threads (glfsx_writer_read_at).
+//     of one; plainFile): read from its current offset to its end by the
+//     library's reader threads with pread(2), straight into the writer's
+//     pinned staging, while earlier batches hash (glfsx_writer_read_fd); the
+//     file is left positioned after what was read, as io.Copy leaves it.
+//   - An *io.SectionReader, *bytes.Reader or *strings.Reader
+//     (positionedReader): the same through ReadAt from several threads
+//     (glfsx_writer_read_at).
 //   - Any other reader fills the staging directly, one Read at a time
 //     (glfsx_writer_reserve / glfsx_writer_commit): every byte is copied
 //     once, by r.Read, instead of into io.Copy's 32 KiB buffer and again by
 //     Write.  C memory handed to Go as a slice is fine under the cgo rules;
 //     it is not used after commit.
 func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
-	if f, ok := r.(osFile); ok {
+	if f, ok := plainFile(r); ok {
 		if st, err := f.Stat(); err == nil && st.Mode().IsRegular() {
 			if pos, err := f.Seek(0, io.SeekCurrent); err == nil {
 				var got C.uint64_t
@@ -259,10 +296,7 @@ func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
 			}
 		}
 	}
-	if ra, ok := r.(interface {
-		io.ReaderAt
-		io.Seeker
-	}); ok {
+	if ra, ok := positionedReader(r); ok {
 		if pos, err := ra.Seek(0, io.SeekCurrent); err == nil {
 			end, err := ra.Seek(0, io.SeekEnd)
 			if err == nil && end >= pos {

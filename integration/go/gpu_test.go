@@ -56,3 +56,48 @@ func TestCreateFromFileTakesFdRoute(t *testing.T) {
 	require.NoError(t, err)
 	require.Equal(t, int64(len(data)), pos) // io.Copy leaves the file at its end
 }
+
+// upperFile embeds *os.File and overrides Read: it has every method the
+// pread route uses (Fd, Stat, Seek, ReadAt), but its bytes are the file's
+// transformed by Read, so ReadFrom must take the generic Read route
+// (ADVICE r5).
+type upperFile struct{ *os.File }
+
+func (u upperFile) Read(p []byte) (int, error) {
+	n, err := u.File.Read(p)
+	for i := range p[:n] {
+		p[i] ^= 0x5a
+	}
+	return n, err
+}
+
+func TestCreateFromFileWrapperUsesItsRead(t *testing.T) {
+	if gpuDeviceCount() == 0 {
+		t.Skip("no GPU")
+	}
+	ctx := context.Background()
+	const maxSize = 1 << 20
+	data := make([]byte, 3*maxSize+77)
+	rand.New(rand.NewSource(2)).Read(data)
+	p := filepath.Join(t.TempDir(), "blob")
+	require.NoError(t, os.WriteFile(p, data, 0o600))
+	xored := make([]byte, len(data))
+	for i, b := range data {
+		xored[i] = b ^ 0x5a
+	}
+
+	ag := NewMachine()
+	want, err := ag.Create(ctx, schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize),
+		nil, bytes.NewReader(xored))
+	require.NoError(t, err)
+
+	f, err := os.Open(p)
+	require.NoError(t, err)
+	defer f.Close()
+	before := atomic.LoadUint64(&fdRouteReads)
+	got, err := ag.Create(ctx, schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize),
+		nil, upperFile{f})
+	require.NoError(t, err)
+	require.Equal(t, before, atomic.LoadUint64(&fdRouteReads), "pread route bypassed Read")
+	require.Equal(t, want.Ref, got.Ref)
+}

@@ -60,7 +60,11 @@ def test_fused_timeout_create_device_repeats(gpu, O, fused_fault):
     assert _create_device(N, t, size, bs)[0] == want       # no fault
     assert fused_fault(0xFFFFFFFF, 0) == before
     fused_fault(5, 2000)
+    # the read-only counter leaves the armed fault in place
+    assert N.lib.glfsx_fused_failures() == before
+    assert N.lib.glfsx_fused_failures() == before
     assert _create_device(N, t, size, bs)[0] == want       # fault, repeated
+    assert N.lib.glfsx_fused_failures() == before + 1
     assert fused_fault(0xFFFFFFFF, 0) == before + 1
     assert _create_device(N, t, size, bs)[0] == want       # flags/counters intact
 

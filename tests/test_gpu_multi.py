@@ -234,3 +234,5 @@ def test_create_devices_config5_level_structure(gpu, O):
     # the gathered level-1 refs posted as the root node (blob.go:184-206)
     idx = O.derive_key(bytes(32), b"index")
     assert O.post(idx, l1.ljust(bs, b"\0"))[0] == root
+    del t
+    torch.cuda.empty_cache()

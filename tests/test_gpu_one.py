@@ -208,3 +208,63 @@ def test_finish_batch_store_error(gpu, O, fail_at):
         w.finish()
     w.close()
     assert [(k, r, c) for k, r, c in log] == [(k, r, c) for k, r, _, c in want[:fail_at]]
+
+
+def test_dropped_result_flag_fails_only_its_call(gpu, O):
+    """a one-shot launch that completes without a request's
+    result flag (what a launch that failed on the device leaves) fails that
+    request's call with GLFSX_E_DEVICE -- and the call returns only once no
+    request of it can still be launched or written, so its stack-held
+    requests are never touched after it returns.  Forced with
+    glfsx_debug_one_drop on a Writer's coalesced few-block post (3 blocks +
+    tail = 4 requests in one call) while 12 other threads post concurrently:
+    exactly that call fails, every other root equals the oracle's, and the
+    poster works afterwards."""
+    from glfs_amd import _native as N
+    bs = 64 << 10
+    data = O.fill_splitmix(3 * bs + 777, 43)
+    want = O.create(data, bs)[0]
+    sink = ctypes.cast(N.lib.glfsx_sink_count, N.POST_FN)
+
+    def create(d):
+        counts, root = (ctypes.c_uint64 * 2)(), N.glfsx_root()
+        rc = N.lib.glfsx_create(bs, bs, None, None, d, len(d), sink, ctypes.byref(counts),
+                                ctypes.byref(root))
+        return rc, bytes(root.ref)
+
+    # alone: request 1 of the call's launch loses its flag
+    N.lib.glfsx_debug_one_drop(1)
+    rc, _ = create(data)
+    assert rc == N.GLFSX_E_DEVICE, rc
+    assert b"without its result flag" in N.lib.glfsx_last_error()
+    assert create(data) == (0, want)
+    # among concurrent callers
+    errors, fails, stop = [], [], threading.Event()
+
+    def worker(t):
+        try:
+            N.check(N.lib.glfsx_set_device(0))
+            rng = random.Random(300 + t)
+            k = 0
+            while not stop.is_set() or k < 10:
+                d = rng.randbytes(rng.choice([9, 4096, 70000, 3 * bs + 5]))
+                rc, r = create(d)
+                if rc == N.GLFSX_E_DEVICE:
+                    fails.append(t)
+                elif rc != 0 or r != O.create(d, bs)[0]:
+                    errors.append((t, rc, len(d)))
+                k += 1
+        except Exception as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    [t.start() for t in th]
+    N.lib.glfsx_debug_one_drop(0)
+    import time
+    time.sleep(0.5)
+    stop.set()
+    [t.join() for t in th]
+    N.lib.glfsx_debug_one_drop(0xFFFFFFFF)
+    assert not errors, errors[:5]
+    assert len(fails) <= 1, fails
+    assert create(data) == (0, want)

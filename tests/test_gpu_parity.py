@@ -522,9 +522,13 @@ def test_config3_64gib_every_ref(gpu, O):
     n0, bf = size // bs, bs // 64
     raw = O.derive_key(bytes(32), b"raw")
     idx = O.derive_key(bytes(32), b"index")
-    free, _ = torch.cuda.mem_get_info()
-    if free < 2 * size + GIB:
-        pytest.skip(f"needs {2 * size + GIB} B of HBM, {free} free")
+    # a card that cannot hold it is a skip; a card that can but has the HBM
+    # held elsewhere is a failure, never a silent skip
+    torch.cuda.empty_cache()
+    free, total = torch.cuda.mem_get_info()
+    if total < 2 * size + GIB:
+        pytest.skip(f"needs {2 * size + GIB} B of HBM, the device has {total}")
+    assert free >= 2 * size + GIB, f"needs {2 * size + GIB} B of HBM, only {free} free"
     t = dev_bytes(torch, size, seed=seed)
     ct = torch.empty(size, dtype=torch.uint8, device="cuda")
     root, posts = _create_device(torch, bs, t, size, ct)

@@ -435,9 +435,9 @@ def _tree_inputs(torch, names, types, modes, sizes, bss):
                                        # last one partial
                                        (40_000, 4 * MIB), (2_500, 128 * 1024)])
 def test_post_tree_device_equals_sequence(gpu, O, n, tree_bs):
-    """glfsx_post_tree_device (blob hashing and tree lines overlapped; tree
-    blocks of 64 KiB spans, at most 64 per block, hashed as the work items
-    of one launch, others by the general post) against the three calls in
+    """glfsx_post_tree_device (blob hashing and tree lines overlapped; the
+    tree blob's blocks posted by the general post, launch_post) against the
+    three calls in
     sequence on the same inputs: ragged blob sizes 0..16 KiB at odd offsets,
     names with JSON escapes and non-ASCII bytes, every blob root, every
     line byte, the tree root."""

@@ -183,20 +183,30 @@ def test_glfs_batch_entry_points_in_both_builds():
 
 
 def test_read_from_matches_io_copy_file_wrapper():
-    """since Go 1.22 io.Copy(w, *os.File) reaches ReadFrom with
-    f.WriteTo's fileWithoutWriteTo wrapper, so the pread route matches an
-    interface the wrapper satisfies (Fd, Stat, Seek), never the concrete
-    *os.File; gpu_test.go (glfsgpu tag) checks through io.Copy that the
-    route is taken."""
+    """since Go 1.22 io.Copy(w, *os.File) reaches ReadFrom
+    with f.WriteTo's fileWithoutWriteTo wrapper, so the pread route takes an
+    *os.File or exactly that wrapper type (plainFile, by dynamic type name);
+    a user type embedding *os.File that overrides Read has the same methods
+    and must NOT match, so nothing is matched by method set.  gpu_test.go
+    (glfsgpu tag) checks both through io.Copy."""
     src = _read("gpu.go")
     body = src[src.index("func (gw *gpuWriter) ReadFrom("):]
     body = body[:body.index("\n}\n")]
-    assert "r.(*os.File)" not in body
-    assert "r.(osFile)" in body and "atomic.AddUint64(&fdRouteReads, 1)" in body
+    assert "r.(osFile)" not in body and "plainFile(r)" in body
+    assert "positionedReader(r)" in body and "io.ReaderAt\n" not in body
+    assert "atomic.AddUint64(&fdRouteReads, 1)" in body
+    pf = src[src.index("func plainFile("):]
+    pf = pf[:pf.index("\n}\n")]
+    assert 'r.(*os.File)' in pf and '"os.fileWithoutWriteTo"' in pf
+    pr = src[src.index("func positionedReader("):]
+    pr = pr[:pr.index("\n}\n")]
+    assert "case *io.SectionReader:" in pr and "case *bytes.Reader:" in pr
     iface = re.search(r"type osFile interface \{([^}]*)\}", src)
     assert iface and "Fd() uintptr" in iface.group(1) and "io.Seeker" in iface.group(1) \
         and "Stat() (os.FileInfo, error)" in iface.group(1)
     test = _read("gpu_test.go")
     assert test.startswith("//go:build glfsgpu\n") and re.search(r"^package bigblob$", test, re.M)
     assert "fdRouteReads" in test and "ag.Create(ctx" in test and 'import "C"' not in test
+    assert "type upperFile struct{ *os.File }" in test
+    assert "TestCreateFromFileWrapperUsesItsRead" in test
     assert test.count("{") == test.count("}") and test.count("(") == test.count(")")
