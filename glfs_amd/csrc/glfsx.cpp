@@ -1264,6 +1264,57 @@ void par_gather(uint8_t *dst, const void *const *blocks, uint64_t k, uint64_t bs
   while (left.load(std::memory_order_acquire) > 0) sched_yield();
 }
 
+// The asynchronous form of par_gather (Concat's slabs): every part goes to
+// the copy pool and *left counts the parts not yet copied; the caller goes
+// on (uploads, decrypts and hashes the previous slab) and waits with
+// gather_wait before it reads dst.  Blocks are copied in runs of consecutive
+// blocks per task, or -- fewer blocks than threads -- in pieces of >= 1 MiB.
+void gather_start(std::atomic<int> *left, uint8_t *dst, const void *const *blocks,
+                  uint64_t k, uint64_t bs, uint64_t last, int dev = -1) {
+  if (k == 0) return;
+  CopyPool &P = copy_pool(dev);
+  const uint64_t total = (k - 1) * bs + last;
+  if (P.workers == 0) {
+    gather_blocks(dst, blocks, k, bs, last);
+    return;
+  }
+  const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>(P.workers, total >> 20));
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (k >= parts) {
+      const uint64_t per = (k + parts - 1) / parts;
+      for (uint64_t b = 0; b < k; b += per) {
+        const uint64_t m = std::min(per, k - b);
+        CopyTask t{};
+        t.dst = dst + b * bs;
+        t.left = left;
+        t.blocks = blocks + b;
+        t.nblk = m;
+        t.bsz = bs;
+        t.lastn = b + m == k ? last : bs;
+        left->fetch_add(1, std::memory_order_relaxed);
+        P.q.push_back(t);
+      }
+    } else {
+      const uint64_t pieces = (parts + k - 1) / k;
+      for (uint64_t i = 0; i < k; ++i) {
+        const uint64_t n = i + 1 == k ? last : bs;
+        const uint64_t per = std::max<uint64_t>(1, ((n / pieces) + 4095) & ~uint64_t(4095));
+        for (uint64_t o = 0; o < n; o += per) {
+          left->fetch_add(1, std::memory_order_relaxed);
+          P.q.push_back({dst + i * bs + o, static_cast<const uint8_t *>(blocks[i]) + o,
+                         size_t(std::min(per, n - o)), left});
+        }
+      }
+    }
+  }
+  P.cv.notify_all();
+}
+
+void gather_wait(std::atomic<int> *left) {
+  while (left->load(std::memory_order_acquire) > 0) sched_yield();
+}
+
 // Read n bytes of input at offset off into dst with the copy pool's threads
 // (pieces of >= 4 MiB, the caller reading the first): an io.ReaderAt / a
 // file read by several threads at once, as a page-cache copy is one core's
@@ -1630,7 +1681,7 @@ int glfsx_clock_probe(int reset, uint64_t out[2]) {
 
 #if GLFSX_WGTIME
 // diagnostic builds only (tools/build_variant.sh): the bulk passes' phase
-// timestamps, 8192 x 8 words
+// timestamps, 8192 x 16 words
 int glfsx_debug_wgtime(uint64_t *out) {
   HIP_TRY(debug_wgtime(out));
   return 0;
@@ -2258,26 +2309,74 @@ int glfsx_writer_write_ctext_blocks(glfsx_writer *w, const void *const *blocks,
     if (int e = w->d_ctx.ensure(slab * block_size + 64)) return e;
     if (int e = w->d_ptx.ensure(slab * block_size + 64)) return e;
     if (int e = w->d_rfx.ensure(64 * slab)) return e;
-    // slab i is gathered into host buffer i & 1 while slab i - 1 uploads,
-    // decrypts and goes into the Writer (all on s_up, in order: the device
-    // temporaries are reused in stream order); buffer i & 1 is free once
-    // slab i - 2's uploads are done
+    // Three stages overlap: the copy threads gather slab i + 1 from the
+    // store's memory into host buffer (i + 1) & 1 while this thread uploads
+    // slab i, decrypts it into the Writer's staging and hands it on (the
+    // Writer's own pipeline hashes it and brings the ctext back); buffer
+    // (i + 1) & 1 is gathered into once slab i - 1's upload from it is done.
+    // Uploads, decrypts and the Writer's copies are in order on s_up (the
+    // device temporaries are reused in stream order).  A -DGLFSX_CONCAT_TRACE=1
+    // build (tools/build_variant.sh) prints each slab's host timeline to
+    // stderr.
     const int dev = w->lanes[0].dev;
-    uint64_t i = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += slab, ++i) {
-      const uint64_t k = std::min(slab, nb - b0);
+    const uint64_t ns = (nb + slab - 1) / slab;
+    std::atomic<int> left[2];
+    left[0].store(0);
+    left[1].store(0);
+    struct Settle {  // no gather may still write a buffer, or read the
+      std::atomic<int> *l;  // caller's blocks, once this call returns
+      ~Settle() {
+        gather_wait(&l[0]);
+        gather_wait(&l[1]);
+      }
+    } settle{left};
+#if GLFSX_CONCAT_TRACE
+    constexpr bool trace = true;
+#else
+    constexpr bool trace = false;
+#endif
+    const auto tz = std::chrono::steady_clock::now();
+    auto us = [&] {
+      return double(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now() - tz).count()) * 1e-3;
+    };
+    std::vector<double> tr;
+    auto start = [&](uint64_t i) {
+      const uint64_t b0 = i * slab, k = std::min(slab, nb - b0);
+      const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
+      gather_start(&left[i & 1], w->h_ctx[i & 1].u8(), blocks + b0, k, block_size,
+                   bytes - (k - 1) * block_size, dev);
+    };
+    start(0);
+    for (uint64_t i = 0; i < ns; ++i) {
+      const uint64_t b0 = i * slab, k = std::min(slab, nb - b0);
       const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
       PinBuf &hb = w->h_ctx[i & 1];
-      if (i >= 2) HIP_TRY(hipEventSynchronize(w->ev_ctx[i & 1]));
-      par_gather(hb.u8(), blocks + b0, k, block_size, bytes - (k - 1) * block_size, dev);
+      const double t_in = trace ? us() : 0;
+      gather_wait(&left[i & 1]);
+      const double t_gathered = trace ? us() : 0;
       memcpy(hb.u8() + bytes, refs + 64 * b0, 64 * k);
       HIP_TRY(hipMemcpyAsync(w->d_ctx.p, hb.p, bytes, hipMemcpyHostToDevice, w->s_up));
       HIP_TRY(hipMemcpyAsync(w->d_rfx.p, hb.u8() + bytes, 64 * k, hipMemcpyHostToDevice,
                              w->s_up));
       HIP_TRY(hipEventRecord(w->ev_ctx[i & 1], w->s_up));
+      double t_next = t_gathered;
+      if (i + 1 < ns) {
+        if (i >= 1) HIP_TRY(hipEventSynchronize(w->ev_ctx[(i + 1) & 1]));
+        t_next = trace ? us() : 0;
+        start(i + 1);
+      }
       HIP_TRY(launch_decrypt(w->d_ctx.u8(), w->d_ptx.u8(), k, block_size,
                              bytes - (k - 1) * block_size, w->d_rfx.u8(), w->s_up));
       if (int e = write_dev(w, w->d_ptx.u8(), bytes)) return e;
+      if (trace) tr.insert(tr.end(), {t_in, t_gathered, t_next, us()});
+    }
+    if (trace) {
+      for (size_t x = 0; x + 3 < tr.size(); x += 4)
+        fprintf(stderr,
+                "concat slab %zu: wait-gather %.1f..%.1f us, next gather from %.1f, "
+                "handed on %.1f\n",
+                x / 4, tr[x], tr[x + 1], tr[x + 2], tr[x + 3]);
     }
     HIP_TRY(hipStreamSynchronize(w->s_up));
     if (w->strict)

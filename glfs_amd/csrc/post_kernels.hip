@@ -971,9 +971,10 @@ __device__ __forceinline__ void tree_merge(uint32_t *lds, uint32_t k, uint32_t t
 #if GLFSX_WGTIME
 // Phase timestamps per workgroup of the bulk passes (A/B diagnostics only,
 // tools/build_variant.sh wgtime "-DGLFSX_WGTIME=1"): [start, chunks done,
-// subtree done, end, HW_ID, XCC_ID, k_pass_dc entry, item fetched]; DEK pass at [0, 4096), CID pass
-// at [4096, 8192).  s_memrealtime: 100 MHz.
-__device__ uint64_t g_wgtime[8192][8];
+// subtree done, end, HW_ID, XCC_ID, k_pass_dc entry, item fetched, DEK wait
+// over (k_pass_dc CID items), 7 spare]; DEK pass at [0, 4096), CID pass at
+// [4096, 8192).  s_memrealtime: 100 MHz.
+__device__ uint64_t g_wgtime[8192][16];
 __device__ __forceinline__ void wgt(bool chacha, uint32_t bid, int slot) {
   const uint32_t b = bid + (chacha ? 4096u : 0u);  // the pass's own workgroup number
   if (threadIdx.x == 0 && b < 8192) {
@@ -1112,6 +1113,9 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
       // saw the epoch (a compiler barrier; the loads are agent-scope, so no
       // cache invalidate is needed)
       __atomic_signal_fence(__ATOMIC_ACQUIRE);
+#if GLFSX_WGTIME
+      if (bid + 4096u < 8192u) g_wgtime[bid + 4096u][8] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         lds[i] = load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i);

@@ -2,7 +2,7 @@
 config 4's small-blob kernels (bench.small_blobs) and the read side
 (batched getF decrypt over a --gib GiB blob at 1 MiB blocks), and config 4
 end to end (bench.config4_end_to_end: blobs, tree lines, tree blob).
-usage: python scripts/legs.py [small|read|both|config4|config4one|config4all|postblob|config2]
+usage: python scripts/legs.py [small|read|both|config4|config4one|config4all|postblob|config2|concat]
        [--gib G]"""
 import ctypes
 import json
@@ -49,6 +49,8 @@ def main():
         out["postblob_concurrency"] = bench.postblob_concurrency(N)
     if what == "config2":
         out["config2"] = bench.config2_leg(torch, N, stream, sp)
+    if what == "concat":       # Concat from a native store (the GLFSX_CONCAT_TRACE build: timeline)
+        out["concat"] = bench.concat_leg(N)
     print(json.dumps(out), flush=True)
 
 

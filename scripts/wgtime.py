@@ -37,7 +37,7 @@ def main():
         N.check(N.lib.glfsx_create_device(bs, None, None, data.data_ptr(), size, ct.data_ptr(),
                                           ctypes.byref(root), ctypes.byref(n_posts), sp))
     s.synchronize()
-    buf = np.zeros((8192, 8), dtype=np.uint64)
+    buf = np.zeros((8192, 16), dtype=np.uint64)
     N.check(fn(buf.ctypes.data))
     out = {}
     for name, base in (("dek", 0), ("cid", 4096)):

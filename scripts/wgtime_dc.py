@@ -43,7 +43,7 @@ def main():
         s.synchronize()
         if rep < 5:
             continue
-        buf = np.zeros((8192, 8), dtype=np.uint64)
+        buf = np.zeros((8192, 16), dtype=np.uint64)
         N.check(fn(buf.ctypes.data))
         rows, kind = [], []
         for k, base in ((0, 0), (1, 4096)):
