@@ -841,9 +841,20 @@ struct OneBuf {
   PinBuf h_in, h_ct, h_ref;  // h_in: one-shot posts of pageable bytes
   int dev = -1;
 };
+// Concat's staging (glfsx_writer_write_ctext_blocks): two pinned slabs the
+// copy threads gather into, the device copy of a slab, its plaintext and its
+// refs.  Pooled per device like the slots: a Concat is one Writer, and
+// allocating and pinning ~130 MiB for each one cost more than the hashing.
+struct CtextBuf {
+  PinBuf h[2];
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  DevBuf d_ctx, d_ptx, d_rfx;
+  int dev = -1;
+};
 std::mutex g_pool_mu;
 std::vector<WSlot> g_slot_pool;
 std::vector<OneBuf> g_one_pool;
+std::vector<CtextBuf> g_ctext_pool;
 struct StreamTriple {
   int dev;
   hipStream_t up, hash, down;
@@ -979,9 +990,8 @@ struct glfsx_writer {
   // device input (write_device / write_ctext): events ordering the caller's
   // stream with the upload stream, and write_ctext's staging / temporaries
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  PinBuf h_ctx[2];            // two slabs: one gathered while the other uploads
-  hipEvent_t ev_ctx[2] = {nullptr, nullptr};
-  DevBuf d_ctx, d_ptx, d_rfx;
+  CtextBuf cx;               // write_ctext's staging (from g_ctext_pool)
+  bool has_cx = false;
   std::vector<WLane> lanes;  // lane 0 = the home device and streams by default
   std::vector<WSlot> slot;   // a ring: slot i runs on lane i % lanes.size()
   int nslots = 3;            // slots per lane
@@ -2301,14 +2311,26 @@ int glfsx_writer_write_ctext_blocks(glfsx_writer *w, const void *const *blocks,
       HIP_TRY(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
     }
-    for (hipEvent_t &ev : w->ev_ctx)
+    if (!w->has_cx) {
+      std::lock_guard<std::mutex> lk(g_pool_mu);
+      for (size_t i = g_ctext_pool.size(); i-- > 0;)
+        if (g_ctext_pool[i].dev == w->dev) {
+          w->cx = g_ctext_pool[i];
+          g_ctext_pool.erase(g_ctext_pool.begin() + i);
+          break;
+        }
+      w->cx.dev = w->dev;
+      w->has_cx = true;
+    }
+    CtextBuf &X = w->cx;
+    for (hipEvent_t &ev : X.ev)
       if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const uint64_t slab = std::max<uint64_t>(1, (64ull << 20) / block_size);
-    for (PinBuf &hb : w->h_ctx)
+    for (PinBuf &hb : X.h)
       if (int e = hb.ensure(slab * block_size + 64 * slab)) return e;
-    if (int e = w->d_ctx.ensure(slab * block_size + 64)) return e;
-    if (int e = w->d_ptx.ensure(slab * block_size + 64)) return e;
-    if (int e = w->d_rfx.ensure(64 * slab)) return e;
+    if (int e = X.d_ctx.ensure(slab * block_size + 64)) return e;
+    if (int e = X.d_ptx.ensure(slab * block_size + 64)) return e;
+    if (int e = X.d_rfx.ensure(64 * slab)) return e;
     // Three stages overlap: the copy threads gather slab i + 1 from the
     // store's memory into host buffer (i + 1) & 1 while this thread uploads
     // slab i, decrypts it into the Writer's staging and hands it on (the
@@ -2344,31 +2366,31 @@ int glfsx_writer_write_ctext_blocks(glfsx_writer *w, const void *const *blocks,
     auto start = [&](uint64_t i) {
       const uint64_t b0 = i * slab, k = std::min(slab, nb - b0);
       const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
-      gather_start(&left[i & 1], w->h_ctx[i & 1].u8(), blocks + b0, k, block_size,
+      gather_start(&left[i & 1], X.h[i & 1].u8(), blocks + b0, k, block_size,
                    bytes - (k - 1) * block_size, dev);
     };
     start(0);
     for (uint64_t i = 0; i < ns; ++i) {
       const uint64_t b0 = i * slab, k = std::min(slab, nb - b0);
       const uint64_t bytes = std::min<uint64_t>(k * block_size, total - b0 * block_size);
-      PinBuf &hb = w->h_ctx[i & 1];
+      PinBuf &hb = X.h[i & 1];
       const double t_in = trace ? us() : 0;
       gather_wait(&left[i & 1]);
       const double t_gathered = trace ? us() : 0;
       memcpy(hb.u8() + bytes, refs + 64 * b0, 64 * k);
-      HIP_TRY(hipMemcpyAsync(w->d_ctx.p, hb.p, bytes, hipMemcpyHostToDevice, w->s_up));
-      HIP_TRY(hipMemcpyAsync(w->d_rfx.p, hb.u8() + bytes, 64 * k, hipMemcpyHostToDevice,
+      HIP_TRY(hipMemcpyAsync(X.d_ctx.p, hb.p, bytes, hipMemcpyHostToDevice, w->s_up));
+      HIP_TRY(hipMemcpyAsync(X.d_rfx.p, hb.u8() + bytes, 64 * k, hipMemcpyHostToDevice,
                              w->s_up));
-      HIP_TRY(hipEventRecord(w->ev_ctx[i & 1], w->s_up));
+      HIP_TRY(hipEventRecord(X.ev[i & 1], w->s_up));
       double t_next = t_gathered;
       if (i + 1 < ns) {
-        if (i >= 1) HIP_TRY(hipEventSynchronize(w->ev_ctx[(i + 1) & 1]));
+        if (i >= 1) HIP_TRY(hipEventSynchronize(X.ev[(i + 1) & 1]));
         t_next = trace ? us() : 0;
         start(i + 1);
       }
-      HIP_TRY(launch_decrypt(w->d_ctx.u8(), w->d_ptx.u8(), k, block_size,
-                             bytes - (k - 1) * block_size, w->d_rfx.u8(), w->s_up));
-      if (int e = write_dev(w, w->d_ptx.u8(), bytes)) return e;
+      HIP_TRY(launch_decrypt(X.d_ctx.u8(), X.d_ptx.u8(), k, block_size,
+                             bytes - (k - 1) * block_size, X.d_rfx.u8(), w->s_up));
+      if (int e = write_dev(w, X.d_ptx.u8(), bytes)) return e;
       if (trace) tr.insert(tr.end(), {t_in, t_gathered, t_next, us()});
     }
     if (trace) {
@@ -2477,12 +2499,26 @@ void glfsx_writer_free(glfsx_writer *w) {
       release_stream_scratch(st);
       (void)hipStreamDestroy(st);
     }
-  for (hipEvent_t ev : {w->ev_in, w->ev_out, w->ev_ctx[0], w->ev_ctx[1]})
+  for (hipEvent_t ev : {w->ev_in, w->ev_out})
     if (ev) (void)hipEventDestroy(ev);
-  for (PinBuf &b : w->h_ctx)
-    if (b.p) (void)hipHostFree(b.p);
-  for (void *p : {w->d_ctx.p, w->d_ptx.p, w->d_rfx.p})
-    if (p) (void)hipFree(p);
+  if (w->has_cx) {  // (its streams are drained above: ev_in is set)
+    bool kept = false;
+    {
+      std::lock_guard<std::mutex> lk(g_pool_mu);
+      if (g_ctext_pool.size() < 4) {
+        g_ctext_pool.push_back(w->cx);
+        kept = true;
+      }
+    }
+    if (!kept) {
+      for (hipEvent_t ev : w->cx.ev)
+        if (ev) (void)hipEventDestroy(ev);
+      for (PinBuf &b : w->cx.h)
+        if (b.p) (void)hipHostFree(b.p);
+      for (void *p : {w->cx.d_ctx.p, w->cx.d_ptx.p, w->cx.d_rfx.p})
+        if (p) (void)hipFree(p);
+    }
+  }
   delete w;
 }
 

@@ -1370,17 +1370,92 @@ __device__ __forceinline__ uint32_t qrot3(uint32_t x) {  // lane q <- lane q+3
   c = c + d;                 \
   b = rotr(b ^ c, 7);
 
+// One round (column step, diagonal step) in quad layout as one asm block
+// (round 6).  tools/chainlat.hip measured the chain's
+// instructions at one wave per SIMD: a dependent v_add/v_xor/v_alignbit
+// chain issues every ~5-8 cycles and the wave as a whole about one VALU
+// instruction per ~4.8 cycles whatever the dependences, so the round costs
+// what it issues.  Here the three row rotations per step change are
+// v_mov_b32_dpp placed where their sources are already two instructions old
+// (no wait states), the diagonal step's first add is split as t = a + m2
+// (issued in the column step) then v_add_u32_dpp a = rot1(b) + t, and one
+// s_nop 0 per step change covers the one DPP read of a just-written b.
+// The compiler's form folded the rotations into the consumers instead and
+// needed ~5.6 wait states per round for them (tools/qchain.hip: 1312 -> 1233
+// cycles per compression with the loads below, 1 wave per SIMD).
+// In: a, b, c, d unrotated (lane q holds column q), t = a + m0, m1..m3.
+//   quad_perm [1,2,3,0]: lane q <- q+1; [2,3,0,1]: q+2; [3,0,1,2]: q+3.
+#define QROUND_ASM                                                              \
+  "v_add_u32 %0, %1, %4\n"                                                      \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 12\n"                                             \
+  "v_add3_u32 %0, %0, %1, %5\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_add_u32 %4, %0, %6\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_mov_b32_dpp %3, %3 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"       \
+  "v_alignbit_b32 %1, %1, %1, 7\n"                                              \
+  "v_mov_b32_dpp %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"       \
+  "s_nop 0\n"                                                                   \
+  "v_add_u32_dpp %0, %1, %4 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_mov_b32_dpp %1, %1 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"       \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 12\n"                                             \
+  "v_add3_u32 %0, %0, %1, %7\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_mov_b32_dpp %3, %3 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"       \
+  "v_alignbit_b32 %1, %1, %1, 7\n"                                              \
+  "v_mov_b32_dpp %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"       \
+  "s_nop 0\n"                                                                   \
+  "v_mov_b32_dpp %1, %1 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"
+
+#ifndef GLFSX_QASM
+#define GLFSX_QASM 1
+#endif
+
 // One compression in quad layout.  addr[4r+k]: LDS byte address of the k-th
 // message word this lane uses in round r.  On return (a, b) = (cv[q], cv[4+q]).
+// Every lane of a quad must be active (the rotations read the other three).
 __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
                                               uint32_t c, uint32_t d,
                                               const uint32_t (&addr)[28]) {
+  typedef const __attribute__((address_space(3))) uint32_t *lw;
+#if GLFSX_QASM
+  // round r+1's four words are read while round r runs
+  uint32_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = *reinterpret_cast<lw>(addr[k]);
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
-    const uint32_t m0 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r]);
-    const uint32_t m1 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 1]);
-    const uint32_t m2 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 2]);
-    const uint32_t m3 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr[4 * r + 3]);
+    uint32_t n[4] = {0, 0, 0, 0};
+    if (r < 6) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) n[k] = *reinterpret_cast<lw>(addr[4 * r + 4 + k]);
+    }
+    uint32_t t = a + m[0];
+    asm volatile(QROUND_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                 : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = n[k];
+  }
+#else
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const uint32_t m0 = *reinterpret_cast<lw>(addr[4 * r]);
+    const uint32_t m1 = *reinterpret_cast<lw>(addr[4 * r + 1]);
+    const uint32_t m2 = *reinterpret_cast<lw>(addr[4 * r + 2]);
+    const uint32_t m3 = *reinterpret_cast<lw>(addr[4 * r + 3]);
     QG(a, b, c, d, m0, m1);
     b = qrot1(b);
     c = qrot2(c);
@@ -1390,6 +1465,7 @@ __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
     c = qrot2(c);
     d = qrot1(d);
   }
+#endif
   a ^= c;
   b ^= d;
 }
@@ -1516,12 +1592,17 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
         blk[b] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
+    // The quad's four lanes are one wave's, and a wave's LDS instructions
+    // are performed in issue order: the compression's reads after the
+    // block's store see it, and the next block's store comes after them, so
+    // neither needs a wait (round 5 waited for both: two LDS round trips
+    // per block on the chain); the empty asm keeps the compiler's order.
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
         *reinterpret_cast<lds_u32x4 *>(slot + 16u * q) =
             u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = a.base;
         if (b == 0) fl |= kChunkStart;
@@ -1531,8 +1612,7 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
         }
         const uint32_t dq = qsel(q, ctr, 0u, blen, fl);
         quad_compress(cl, ch, ivq, dq, addr);
-        // the slot is rewritten next block: reads of this block are done
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
       }
     }
   }
@@ -1808,6 +1888,22 @@ __device__ __forceinline__ void one_store(const uint4 *img_u4, uint8_t *dst, uin
   }
 }
 
+// The descriptor, staged into LDS by one load per word, all issued at once
+// (round 6).  It lives in pinned host memory, and reading its fields where
+// they are used made each group of them a PCIe round trip (~1.7 us) on the
+// post's critical path: round 5's k_one waited for the salt words after the
+// message, then for the CID key, the output pointers, the flag and the
+// sequence number (s_load ... s_waitcnt pairs in the code object).
+__device__ __forceinline__ const OneDesc *one_desc(OneDesc *s, const OneDesc *g) {
+  constexpr uint32_t kW = sizeof(OneDesc) / 4;
+  static_assert(sizeof(OneDesc) % 4 == 0 && kW <= 64, "wave 0 stages the descriptor");
+  if (threadIdx.x < kW)
+    reinterpret_cast<uint32_t *>(s)[threadIdx.x] =
+        reinterpret_cast<const uint32_t *>(g)[threadIdx.x];
+  __syncthreads();
+  return s;
+}
+
 // The post's results (ctext, ref) are in the caller's staging: every lane's
 // stores are done, then one release store of the descriptor's sequence
 // number into its flag (pinned host memory) tells the waiting caller, with
@@ -1846,8 +1942,9 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
   __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_dek[8];
+  __shared__ OneDesc s_desc;
   constexpr int kLanes = QUADS * 4;
-  const OneDesc *dp = descs + blockIdx.x;
+  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x);
   const uint32_t len = dp->len;
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
@@ -1941,7 +2038,8 @@ __global__ __launch_bounds__(256) void k_med_dek(const OneDesc *descs, uint32_t 
   __shared__ uint4 ts_u4[32 * 4];
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_flag;
-  const OneDesc *dp = descs + blockIdx.x / wmax;
+  __shared__ OneDesc s_desc;
+  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x / wmax);
   const uint32_t sidx = blockIdx.x % wmax;
   const uint32_t len = dp->len;
   const uint32_t W = (len + 65535u) >> 16;
@@ -1976,7 +2074,8 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
   __shared__ uint4 ts_u4[32 * 4];
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_flag;
-  const OneDesc *dp = descs + blockIdx.x / wmax;
+  __shared__ OneDesc s_desc;
+  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x / wmax);
   const uint32_t sidx = blockIdx.x % wmax;
   const uint32_t len = dp->len;
   const uint32_t W = (len + 65535u) >> 16;

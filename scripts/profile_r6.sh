@@ -2,6 +2,8 @@
 # Round-6 measurements behind profiles/r6/ (run on the GPU box from the repo root):
 #   chainlat : dependent-issue latency of the quad chain's instructions
 #              (tools/chainlat, one wave per SIMD)
+#   qchain   : the quad compression chain itself, product form vs hand-
+#              scheduled asm rounds (tools/qchain.hip), 1 and 4 waves per SIMD
 #   c2_attrib: config 2's one-launch post split into ramp / prologue / DEK
 #              wait / body / drain, beside the headline kernels' per-byte body
 #              time (GLFSX_WGTIME build, scripts/c2_attrib.py)
@@ -17,6 +19,8 @@ SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_
 C2="python bench.py --no-extras --size-gib 1 --block-size 2097152 --steps 10 --warmup 2"
 HL="python bench.py --no-extras --steps 3 --warmup 1"
 timeout -k 10 60 ./tools/chainlat > $OUT/chainlat.json 2> $OUT/chainlat.err || exit $?
+timeout -k 10 60 ./tools/qchain 256 256 > $OUT/qchain_1wave.json 2> $OUT/qchain.err || exit $?
+timeout -k 10 60 ./tools/qchain 256 1024 > $OUT/qchain_4wave.json 2>> $OUT/qchain.err || exit $?
 GLFSX_LIB=glfs_amd/libglfsx_wgtime.so timeout -k 10 200 python scripts/c2_attrib.py 3 > $OUT/c2_attrib.json 2> $OUT/c2_attrib.err || exit $?
 timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace -f csv -d $OUT/c2_sq -o run -- $C2 > $OUT/c2_sq.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/c2_fetch -o run -- $C2 > $OUT/c2_fetch.log 2>&1 || exit $?
