@@ -1894,7 +1894,11 @@ __device__ __forceinline__ void one_store(const uint4 *img_u4, uint8_t *dst, uin
 // post's critical path: round 5's k_one waited for the salt words after the
 // message, then for the CID key, the output pointers, the flag and the
 // sequence number (s_load ... s_waitcnt pairs in the code object).
+#ifndef GLFSX_DESC_LDS
+#define GLFSX_DESC_LDS 1
+#endif
 __device__ __forceinline__ const OneDesc *one_desc(OneDesc *s, const OneDesc *g) {
+  if (!GLFSX_DESC_LDS) return g;  // (A/B builds: fields read where used)
   constexpr uint32_t kW = sizeof(OneDesc) / 4;
   static_assert(sizeof(OneDesc) % 4 == 0 && kW <= 64, "wave 0 stages the descriptor");
   if (threadIdx.x < kW)

@@ -110,43 +110,73 @@ var (
 	parityEvery = envInt("GLFSX_PARITY", 0)
 	strict      = envInt("GLFSX_STRICT", 0)
 	devices     = envInts("GLFSX_DEVICES")
+	// A blob shorter than this (and than one block) never reaches the GPU:
+	// the reference's own Go path posts it.  One PostBlob per small file
+	// (glfsposix, glfstar) is ~7x cheaper on a CPU core than a GPU call --
+	// 4 KiB: 149 k blobs/s against 22 k calls/s from one thread, 2.39 M
+	// against 0.23 M from 16 (bench cpu_baseline.small_blobs,
+	// postblob_concurrency) -- and the crossover is ~32-48 KiB (DESIGN.md
+	// section 11).  0 sends every blob to the GPU.
+	gpuMinBytes = envInt("GLFSX_GPU_MIN_BYTES", 32<<10)
 )
 
+// gpuStarts counts writers that reached the GPU (gpu_test.go).
+var gpuStarts uint64
+
+// gpuWriter is the GPU half of a bigblob Writer.  It holds the bytes of a
+// blob in the Writer's own buf until they reach minBytes; only then is the
+// library's writer created (start) and the buffered bytes handed to it, so
+// a blob that ends first is finished by blob.go's Go path with the same
+// Posts (the GPU path's Posts are the reference's; tests/test_gpu_*).
 type gpuWriter struct {
-	w   *C.glfsx_writer
-	s   bcsdk.WO
-	ctx context.Context
-	err error // the store's error, returned by the Write/Finish that saw it
-	h   cgo.Handle
-	n   uint64
+	w        *C.glfsx_writer // nil until start
+	ag       *Machine
+	s        bcsdk.WO
+	salt     [32]byte
+	minBytes int
+	ctx      context.Context
+	err      error // the store's error, returned by the Write/Finish that saw it
+	h        cgo.Handle
+	n        uint64
 }
 
-// newGPUWriter mirrors blob.go:85-114 (NewWriter): block size 0 means the
-// store's MaxSize (bigblob machine.go:22-30), a nil salt is 0^32.
-func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte) *Writer {
+// newGPUWriter is called by NewWriter (blob.go:85-114) after the reference's
+// checks: blockSize is the one it chose, salt the one it uses (never nil).
+func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte, blockSize int) *gpuWriter {
 	if C.glfsx_device_count() == 0 {
 		return nil // no GPU: the Go path (the library has no CPU fallback)
 	}
-	gw := &gpuWriter{s: s, ctx: context.TODO()}
-	gw.h = cgo.NewHandle(gw)
-	var csalt *C.uint8_t
+	gw := &gpuWriter{ag: ag, s: s, ctx: context.TODO(), minBytes: gpuMinBytes}
 	if salt != nil {
-		csalt = (*C.uint8_t)(unsafe.Pointer(&salt[0])) // read during the call only
+		gw.salt = *salt
 	}
+	if blockSize < gw.minBytes {
+		gw.minBytes = blockSize // the reference posts its first block there
+	}
+	return gw
+}
+
+func (gw *gpuWriter) started() bool { return gw.w != nil }
+
+// start creates the library's writer and hands it the bytes buffered so
+// far (*buf, emptied).  blob.go:85-114 (NewWriter): block size 0 means the
+// store's MaxSize (bigblob machine.go:22-30).
+func (gw *gpuWriter) start(buf *[]byte) error {
+	if gw.w != nil {
+		return nil
+	}
+	gw.h = cgo.NewHandle(gw)
 	var rc C.int
 	var cerr [512]C.char
-	gw.w = C.writer_new(C.uint64_t(ag.blockSize), C.uint64_t(s.MaxSize()), csalt,
-		C.uintptr_t(gw.h), &rc, &cerr[0], C.size_t(len(cerr)))
+	gw.w = C.writer_new(C.uint64_t(gw.ag.blockSize), C.uint64_t(gw.s.MaxSize()),
+		(*C.uint8_t)(unsafe.Pointer(&gw.salt[0])), C.uintptr_t(gw.h), &rc, &cerr[0],
+		C.size_t(len(cerr)))
 	if gw.w == nil {
 		gw.h.Delete()
-		msg := C.GoString(&cerr[0])
-		switch rc {
-		case C.GLFSX_E_BLOCKSIZE_GT_MAX, C.GLFSX_E_BLOCKSIZE_LT_MIN:
-			panic(msg) // blob.go:91 "blockSize %d > maxSize %d", :94 "blockSize cannot be < 128"
-		default:
-			panic(fmt.Errorf("glfsx %d: %s", int(rc), msg))
-		}
+		// (the block-size panics of blob.go:91,94 happened in NewWriter)
+		return fmt.Errorf("glfsx %d: %s", int(rc), C.GoString(&cerr[0]))
 	}
+	atomic.AddUint64(&gpuStarts, 1)
 	C.glfsx_writer_set_strict(gw.w, C.int(strict))
 	if len(devices) > 0 {
 		cdevs := (*C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))
@@ -158,10 +188,56 @@ func (ag *Machine) newGPUWriter(s bcsdk.WO, salt *[32]byte) *Writer {
 		if rc := C.writer_devices(gw.w, cdevs, C.int(len(devices)), &cerr[0],
 			C.size_t(len(cerr))); rc != 0 {
 			gw.close()
-			panic(fmt.Errorf("glfsx %d: %s", int(rc), C.GoString(&cerr[0])))
+			return fmt.Errorf("glfsx %d: %s", int(rc), C.GoString(&cerr[0]))
 		}
 	}
-	return &Writer{gpu: gw}
+	if len(*buf) > 0 {
+		if _, err := gw.Write(*buf); err != nil {
+			return err
+		}
+		*buf = (*buf)[:0]
+	}
+	return nil
+}
+
+// write is Writer.Write (blob.go:120-133) on this path: below minBytes the
+// bytes wait in the Writer's buf, as the reference's do below a block.
+func (gw *gpuWriter) write(buf *[]byte, data []byte) (int, error) {
+	if gw.w == nil && len(*buf)+len(data) < gw.minBytes {
+		*buf = append(*buf, data...)
+		return len(data), nil
+	}
+	if err := gw.start(buf); err != nil {
+		return 0, err
+	}
+	return gw.Write(data)
+}
+
+// readFrom is Writer.ReadFrom: the first minBytes are read into buf (a
+// blob that ends there stays on the Go path), the rest by ReadFrom below.
+func (gw *gpuWriter) readFrom(buf *[]byte, r io.Reader) (int64, error) {
+	var n int64
+	for gw.w == nil && len(*buf) < gw.minBytes {
+		if cap(*buf) < gw.minBytes {
+			b := make([]byte, len(*buf), gw.minBytes)
+			copy(b, *buf)
+			*buf = b
+		}
+		k, err := r.Read((*buf)[len(*buf):gw.minBytes])
+		*buf = (*buf)[:len(*buf)+k]
+		n += int64(k)
+		if err == io.EOF {
+			return n, nil
+		}
+		if err != nil {
+			return n, err
+		}
+	}
+	if err := gw.start(buf); err != nil {
+		return n, err
+	}
+	m, err := gw.ReadFrom(r)
+	return n + m, err
 }
 
 //export goPost

@@ -15,8 +15,11 @@ import (
 
 type gpuWriter struct{ ctx context.Context }
 
-func (gw *gpuWriter) Write([]byte) (int, error)             { panic("unreachable") }
-func (gw *gpuWriter) ReadFrom(io.Reader) (int64, error)     { panic("unreachable") }
-func (gw *gpuWriter) Finish(context.Context) (*Root, error) { panic("unreachable") }
+func (gw *gpuWriter) started() bool                            { panic("unreachable") }
+func (gw *gpuWriter) write(*[]byte, []byte) (int, error)       { panic("unreachable") }
+func (gw *gpuWriter) readFrom(*[]byte, io.Reader) (int64, error) { panic("unreachable") }
+func (gw *gpuWriter) Write([]byte) (int, error)                { panic("unreachable") }
+func (gw *gpuWriter) ReadFrom(io.Reader) (int64, error)        { panic("unreachable") }
+func (gw *gpuWriter) Finish(context.Context) (*Root, error)    { panic("unreachable") }
 
-func (ag *Machine) newGPUWriter(bcsdk.WO, *[32]byte) *Writer { return nil }
+func (ag *Machine) newGPUWriter(bcsdk.WO, *[32]byte, int) *gpuWriter { return nil }

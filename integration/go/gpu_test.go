@@ -101,3 +101,43 @@ func TestCreateFromFileWrapperUsesItsRead(t *testing.T) {
 	require.Equal(t, before, atomic.LoadUint64(&fdRouteReads), "pread route bypassed Read")
 	require.Equal(t, want.Ref, got.Ref)
 }
+
+// A blob below GLFSX_GPU_MIN_BYTES (and below one block) never reaches the
+// GPU: the reference's Go path posts it, with the root the GPU path gives
+// for the same bytes; a blob at the threshold starts the library's writer.
+func TestSmallBlobStaysOnGoPath(t *testing.T) {
+	if gpuDeviceCount() == 0 {
+		t.Skip("no GPU")
+	}
+	ctx := context.Background()
+	const maxSize = 1 << 20
+	ag := NewMachine()
+	for _, n := range []int{0, 1, 4096, gpuMinBytes - 1, gpuMinBytes, 3*maxSize + 5} {
+		data := make([]byte, n)
+		rand.New(rand.NewSource(int64(n))).Read(data)
+		before := atomic.LoadUint64(&gpuStarts)
+		got, err := ag.Create(ctx, schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize),
+			nil, bytes.NewReader(data))
+		require.NoError(t, err)
+		started := atomic.LoadUint64(&gpuStarts) - before
+		if n < gpuMinBytes {
+			require.Equal(t, uint64(0), started, "blob of %d bytes reached the GPU", n)
+		} else {
+			require.Equal(t, uint64(1), started, "blob of %d bytes did not reach the GPU", n)
+		}
+		// the same bytes written in pieces: same root either way
+		w := ag.NewWriter(schema.NewMem(blobcache.HashAlgo_BLAKE3_256.HashFunc(), maxSize), nil)
+		for off := 0; off < n; off += 1000 {
+			end := off + 1000
+			if end > n {
+				end = n
+			}
+			_, err := w.Write(data[off:end])
+			require.NoError(t, err)
+		}
+		got2, err := w.Finish(ctx)
+		require.NoError(t, err)
+		require.Equal(t, got.Ref, got2.Ref)
+		require.Equal(t, uint64(n), got.Size)
+	}
+}

@@ -39,20 +39,27 @@ def test_patch_hooks_exist_in_both_builds():
     patch = _read("bigblob_gpu.patch")
     added = "\n".join(ln[1:] for ln in patch.splitlines()
                       if ln.startswith("+") and not ln.startswith("+++"))
-    assert "ag.newGPUWriter(s, salt)" in added
-    assert "w.gpu.Write(data)" in added and "w.gpu.Finish(ctx)" in added
+    assert "w.gpu = ag.newGPUWriter(s, salt, blockSize)" in added
+    assert "w.gpu.write(&w.buf, data)" in added and "w.gpu.Finish(ctx)" in added
     assert "w.gpu.ctx = ctx" in added and "gpu *gpuWriter" in added
-    assert "return w.gpu.ReadFrom(r)" in added and "io.Copy(writerOnly{w}, r)" in added
+    assert "return w.gpu.readFrom(&w.buf, r)" in added and "io.Copy(writerOnly{w}, r)" in added
+    # round 6: a writer that never reached the GPU finishes on the Go path
+    assert "if w.gpu.started() {" in added and "w.gpu = nil" in added
     # context lines are the reference's own (blob.go:85-86)
     assert " func (ag *Machine) NewWriter(s bcsdk.WO, salt *[32]byte) *Writer {" in patch
-    assert " \tblockSize := s.MaxSize()" in patch
+    assert "-\treturn &Writer{" in patch and "+\tw := &Writer{" in patch
     for name, tag in (("gpu.go", "//go:build glfsgpu"), ("gpu_stub.go", "//go:build !glfsgpu")):
         src = _read(name)
         assert src.startswith(tag + "\n"), name
         assert re.search(r"^package bigblob$", src, re.M), name
         assert re.search(r"type gpuWriter struct\s*\{[^}]*\bctx\s+context\.Context", src, re.S), name
-        assert re.search(r"func \(ag \*Machine\) newGPUWriter\((s )?bcsdk\.WO, (salt )?\*\[32\]byte\) "
-                         r"\*Writer", src), name
+        assert re.search(r"func \(ag \*Machine\) newGPUWriter\((s )?bcsdk\.WO, (salt )?\*\[32\]byte, "
+                         r"(blockSize )?int\) \*gpuWriter", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) started\(\) bool", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) write\((buf )?\*\[\]byte, (data )?\[\]byte\) "
+                         r"\(int, error\)", src), name
+        assert re.search(r"func \(gw \*gpuWriter\) readFrom\((buf )?\*\[\]byte, (r )?io\.Reader\) "
+                         r"\(int64, error\)", src), name
         assert re.search(r"func \(gw \*gpuWriter\) Write\((data )?\[\]byte\) \(int, error\)", src), name
         assert re.search(r"func \(gw \*gpuWriter\) Finish\((ctx )?context\.Context\) "
                          r"\(\*Root, error\)", src), name
