@@ -1061,6 +1061,47 @@ __device__ __forceinline__ void publish_dek(uint8_t *dst, const uint32_t (&w)[8]
     __hip_atomic_store(c->ready + j, d.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A CID item's wait for its message's DEK (k_pass_dc): from the DEK work
+// items of the same launch.  Work items are taken from work lists
+// (k_pass_dc), so every DEK item was taken by a workgroup that was already
+// running before this one took its CID item: the wait depends only on
+// running workgroups, whatever the dispatch order or other launches sharing
+// the chip.  It is bounded anyway; a timeout marks the launch failed in
+// d.err (the host then discards its results) and the workgroup finishes
+// with whatever key it read, so counters and flags stay consistent for later
+// launches.  Every thread of the workgroup calls it; dek is uniform.
+__device__ __forceinline__ void dc_dek_wait(const DcState *dc, uint64_t j, uint32_t bid,
+                                            const uint8_t *ref, uint32_t *lds,
+                                            uint32_t (&dek)[8]) {
+  (void)bid;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const DcConst *c = dc->c;  // (the DEK items this one waits for precede it in its list)
+    while (__hip_atomic_load(c->ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+           dc->epoch) {
+      __builtin_amdgcn_s_sleep(4);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > c->wait_ticks) {
+        __hip_atomic_store(c->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    // the DEK loads below must not be hoisted above the flag load that
+    // saw the epoch (a compiler barrier; the loads are agent-scope, so no
+    // cache invalidate is needed)
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);
+#if GLFSX_WGTIME
+    if (bid + 4096u < 8192u) g_wgtime[bid + 4096u][8] = __builtin_amdgcn_s_memrealtime();
+#endif
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      lds[i] = load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dek[i] = __builtin_amdgcn_readfirstlane(lds[i]);
+  __syncthreads();
+}
+
 // The body of one workgroup (number bid) of a pass.  FUSE: 0 = a pass of its
 // own; 1 = the DEK part of k_pass_dc (publishes each DEK with its ready
 // flag); 2 = the CID part (waits for its message's DEK).
@@ -1090,40 +1131,7 @@ __device__ __forceinline__ void pass_body(const KArgs &a, uint32_t bid, uint4 *l
   for (int i = 0; i < 8; ++i) key[i] = a.key[i];
   uint32_t dek[8];
   if constexpr (FUSE == 2) {
-    // this message's DEK, from the DEK work items of the same launch.  Work
-    // items are taken from work lists (k_pass_dc), so every DEK item was taken by
-    // a workgroup that was already running before this one took its CID
-    // item: the wait depends only on running workgroups, whatever the
-    // dispatch order or other launches sharing the chip.  It is bounded
-    // anyway; a timeout marks the launch failed in d.err (the host then
-    // discards its results) and the workgroup finishes with whatever key it
-    // read, so counters and flags stay consistent for later launches.
-    if (t == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const DcConst *c = dc->c;  // (the DEK items this one waits for precede it in its list)
-      while (__hip_atomic_load(c->ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-             dc->epoch) {
-        __builtin_amdgcn_s_sleep(4);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > c->wait_ticks) {
-          __hip_atomic_store(c->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      // the DEK loads below must not be hoisted above the flag load that
-      // saw the epoch (a compiler barrier; the loads are agent-scope, so no
-      // cache invalidate is needed)
-      __atomic_signal_fence(__ATOMIC_ACQUIRE);
-#if GLFSX_WGTIME
-      if (bid + 4096u < 8192u) g_wgtime[bid + 4096u][8] = __builtin_amdgcn_s_memrealtime();
-#endif
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        lds[i] = load_cv_word(reinterpret_cast<const uint32_t *>(ref + 32) + i);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dek[i] = __builtin_amdgcn_readfirstlane(lds[i]);
-    __syncthreads();
+    dc_dek_wait(dc, j, bid, ref, lds, dek);
   } else if constexpr (CHACHA) {
     // DEK written by the preceding pass into bytes [32,64) of this ref slot.
     const uint8_t *dp = ref + 32;
@@ -1427,21 +1435,24 @@ __device__ __forceinline__ uint32_t qrot3(uint32_t x) {  // lane q <- lane q+3
 // One compression in quad layout.  addr[4r+k]: LDS byte address of the k-th
 // message word this lane uses in round r.  On return (a, b) = (cv[q], cv[4+q]).
 // Every lane of a quad must be active (the rotations read the other three).
-__device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
-                                              uint32_t c, uint32_t d,
-                                              const uint32_t (&addr)[28]) {
-  typedef const __attribute__((address_space(3))) uint32_t *lw;
-#if GLFSX_QASM
-  // round r+1's four words are read while round r runs
-  uint32_t m[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) m[k] = *reinterpret_cast<lw>(addr[k]);
+// quad_compress_m: m holds round 0's four words, already read; with PF, the
+// four words at nxt (the next compression's round 0) are read during round 6
+// and left in m, so a chain of compressions over a static LDS image waits
+// for LDS only once (k_one).
+typedef const __attribute__((address_space(3))) uint32_t *lds_word;
+template <bool PF>
+__device__ __forceinline__ void quad_compress_m(uint32_t &a, uint32_t &b, uint32_t c,
+                                                uint32_t d, const uint32_t (&addr)[28],
+                                                uint32_t (&m)[4], const uint32_t *nxt) {
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
     uint32_t n[4] = {0, 0, 0, 0};
     if (r < 6) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) n[k] = *reinterpret_cast<lw>(addr[4 * r + 4 + k]);
+      for (int k = 0; k < 4; ++k) n[k] = *reinterpret_cast<lds_word>(addr[4 * r + 4 + k]);
+    } else if (PF) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) n[k] = *reinterpret_cast<lds_word>(nxt[k]);
     }
     uint32_t t = a + m[0];
     asm volatile(QROUND_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
@@ -1449,13 +1460,26 @@ __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
 #pragma unroll
     for (int k = 0; k < 4; ++k) m[k] = n[k];
   }
+  a ^= c;
+  b ^= d;
+}
+
+__device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
+                                              uint32_t c, uint32_t d,
+                                              const uint32_t (&addr)[28]) {
+#if GLFSX_QASM
+  // round r+1's four words are read while round r runs
+  uint32_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = *reinterpret_cast<lds_word>(addr[k]);
+  quad_compress_m<false>(a, b, c, d, addr, m, nullptr);
 #else
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
-    const uint32_t m0 = *reinterpret_cast<lw>(addr[4 * r]);
-    const uint32_t m1 = *reinterpret_cast<lw>(addr[4 * r + 1]);
-    const uint32_t m2 = *reinterpret_cast<lw>(addr[4 * r + 2]);
-    const uint32_t m3 = *reinterpret_cast<lw>(addr[4 * r + 3]);
+    const uint32_t m0 = *reinterpret_cast<lds_word>(addr[4 * r]);
+    const uint32_t m1 = *reinterpret_cast<lds_word>(addr[4 * r + 1]);
+    const uint32_t m2 = *reinterpret_cast<lds_word>(addr[4 * r + 2]);
+    const uint32_t m3 = *reinterpret_cast<lds_word>(addr[4 * r + 3]);
     QG(a, b, c, d, m0, m1);
     b = qrot1(b);
     c = qrot2(c);
@@ -1465,9 +1489,9 @@ __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,
     c = qrot2(c);
     d = qrot1(d);
   }
-#endif
   a ^= c;
   b ^= d;
+#endif
 }
 
 __device__ __forceinline__ uint32_t qsel(uint32_t q, uint32_t x0, uint32_t x1,
@@ -1475,9 +1499,11 @@ __device__ __forceinline__ uint32_t qsel(uint32_t q, uint32_t x0, uint32_t x1,
   return q == 0 ? x0 : q == 1 ? x1 : q == 2 ? x2 : x3;
 }
 
-// The 28 LDS addresses of a 64-B slot at byte `slot` for lane q.
+// The 28 LDS addresses of a 64-B slot at byte `slot` for lane q; with x
+// (a multiple of 4), word w of the slot lives at word w ^ x (the block
+// slots of k_quad, below).
 __device__ __forceinline__ void quad_addrs(uint32_t (&addr)[28], uint32_t slot,
-                                           uint32_t q) {
+                                           uint32_t q, uint32_t x = 0) {
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
     constexpr int kk[4] = {0, 1, 8, 9};
@@ -1485,7 +1511,7 @@ __device__ __forceinline__ void quad_addrs(uint32_t (&addr)[28], uint32_t slot,
     for (int k = 0; k < 4; ++k) {
       const uint32_t w = qsel(q, kSched.s[r][kk[k]], kSched.s[r][kk[k] + 2],
                               kSched.s[r][kk[k] + 4], kSched.s[r][kk[k] + 6]);
-      addr[4 * r + k] = slot + 4u * w;
+      addr[4 * r + k] = slot + 4u * (w ^ x);
     }
   }
 }
@@ -1553,7 +1579,12 @@ __device__ __forceinline__ void tree_reduce_q(uint32_t *lds, uint32_t k, uint32_
 // CUs instead of 8).
 template <int QPW>
 __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
-  __shared__ uint4 slots[QPW * 4];      // 64 B message slot per quad
+  // Block slots of the chunk phase: one 64-B slot per quad; QPW = 64 has a
+  // second set QPW x 64 B further on (block b+1 is stored while block b
+  // compresses, and its first words are read in block b's last round).
+  // The subtree merges use the first set's 64-B slots as parent slots.
+  constexpr bool kTwo = QPW == 64;
+  __shared__ uint4 slots[QPW * (kTwo ? 8 : 4)];
   __shared__ uint32_t passbuf[8];       // the odd subtree passing up a level
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint64_t j = blockIdx.x >> a.split_log2;
@@ -1593,15 +1624,48 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
       }
     }
     // The quad's four lanes are one wave's, and a wave's LDS instructions
-    // are performed in issue order: the compression's reads after the
-    // block's store see it, and the next block's store comes after them, so
-    // neither needs a wait (round 5 waited for both: two LDS round trips
-    // per block on the chain); the empty asm keeps the compiler's order.
+    // are performed in issue order: a compression's reads after its
+    // block's store see it, and a later store into the slot comes after
+    // them, so neither needs a wait (round 5 waited for both: two LDS round
+    // trips per block on the chain); the empty asm keeps the compiler's
+    // order.
+    // Block slots are word-swizzled: word w of quad i's slot sits at word
+    // w ^ x_i, x_i = 4 ((i >> 1) & 3), so the eight quads of a 32-lane LDS
+    // group (ds_read_b32 banks = word mod 32) reading the same word hit
+    // eight banks instead of two (plain 64-B slots: 4-way conflicts on every
+    // message read); a lane's 16-B block store stays one aligned granule.
+    // (QPW = 256 keeps plain slots: a second 28-address set would spill the
+    // 1024-lane workgroup's 128 registers)
+    const uint32_t x = kTwo ? 4u * ((quad >> 1) & 3u) : 0u;
+    const uint32_t gq = 16u * (q ^ (x >> 2));  // this lane's granule in a slot
+    constexpr uint32_t kB = kTwo ? QPW * 64u : 0u;  // the second slot set
+    uint32_t caddr[28];
+    if constexpr (kTwo) {
+      quad_addrs(caddr, slot, q, x);
+#pragma unroll
+      for (int k = 0; k < 28; ++k) asm volatile("" : "+v"(caddr[k]));  // kept, not rebuilt per read
+    }
+    uint32_t m[4];
+    if constexpr (kTwo) {
+      *reinterpret_cast<lds_u32x4 *>(slot + gq) =
+          u32x4{blk[0].x, blk[0].y, blk[0].z, blk[0].w};
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m[k] = *reinterpret_cast<lds_word>(caddr[k]);
+    }
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
-        *reinterpret_cast<lds_u32x4 *>(slot + 16u * q) =
-            u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
+        const bool more = uint32_t(b) + 1 < nb;
+        if constexpr (kTwo) {
+          if (b + 1 < 16 && more)
+            *reinterpret_cast<lds_u32x4 *>(slot + kB * ((b + 1) & 1) + gq) =
+                u32x4{blk[(b + 1) & 15].x, blk[(b + 1) & 15].y, blk[(b + 1) & 15].z,
+                      blk[(b + 1) & 15].w};
+        } else {
+          *reinterpret_cast<lds_u32x4 *>(slot + gq) =
+              u32x4{blk[b].x, blk[b].y, blk[b].z, blk[b].w};
+        }
         asm volatile("" ::: "memory");
         const uint32_t blen = min(clen - min(clen, 64u * b), 64u);
         uint32_t fl = a.base;
@@ -1611,7 +1675,17 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
           if (whole && cnt == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr, 0u, blen, fl);
-        quad_compress(cl, ch, ivq, dq, addr);
+        if constexpr (kTwo) {
+          uint32_t ab[28], nxt[4];
+#pragma unroll
+          for (int k = 0; k < 28; ++k) ab[k] = caddr[k] + kB * (b & 1);
+          const uint32_t noff = more ? kB * ((b + 1) & 1) : kB * (b & 1);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nxt[k] = caddr[k] + noff;
+          quad_compress_m<true>(cl, ch, ivq, dq, ab, m, nxt);
+        } else {
+          quad_compress(cl, ch, ivq, dq, addr);
+        }
         asm volatile("" ::: "memory");
       }
     }
@@ -1720,6 +1794,14 @@ __global__ __launch_bounds__(QPW * 4) void k_quad(KArgs a) {
 // Messages of up to kMaxMedLen bytes span several such workgroups (64 KiB
 // each) in two launches, k_med_dek and k_med_cid (below).
 
+// The one-shot image's 16-B granules are swizzled per 1 KiB chunk: granule
+// g sits at g ^ ((g >> 6) & 3), i.e. word w of a chunk c's block at word
+// w ^ 4 (c & 3) of that block.  The quads of a 32-lane LDS group read the
+// same word of their chunks (1 KiB apart, so one bank unswizzled: 4-way at
+// 4 KiB, 8-way at 16 KiB and up); swizzled it is 2-way at most.  Every
+// access to the image goes through img_g.
+__device__ __forceinline__ uint32_t img_g(uint32_t g) { return g ^ ((g >> 6) & 3u); }
+
 // Quad `quad` hashes chunk `quad` of the image (len bytes from the image
 // start; chunk counter ctr0 + quad); root: the image is the whole message.
 __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t img,
@@ -1733,9 +1815,18 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
   if (quad < C) {
     const uint32_t clen = min(len - min(len, quad << 10), 1024u);
     const uint32_t nb = clen ? (clen + 63) >> 6 : 1u;
+    // the chunk's 28 word addresses once (opaque to the optimiser, which
+    // otherwise rebuilt each from the lane's offset with an add per read);
+    // block b's reads carry its 64 b as the instruction offset
     uint32_t addr[28];
 #pragma unroll
-    for (int k = 0; k < 28; ++k) addr[k] = img + (quad << 10) + rel[k];
+    for (int k = 0; k < 28; ++k) {
+      addr[k] = img + (quad << 10) + (rel[k] ^ (16u * (quad & 3u)));  // (img_g)
+      asm volatile("" : "+v"(addr[k]));
+    }
+    uint32_t m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = *reinterpret_cast<lds_word>(addr[k]);
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
       if (uint32_t(b) < nb) {
@@ -1747,10 +1838,14 @@ __device__ __forceinline__ void one_chunks(uint32_t &cl, uint32_t &ch, uint32_t 
           if (root && C == 1) fl |= kRoot;
         }
         const uint32_t dq = qsel(q, ctr0 + quad, 0u, blen, fl);
-        uint32_t ab[28];
+        uint32_t ab[28], nxt[4];
 #pragma unroll
         for (int k = 0; k < 28; ++k) ab[k] = addr[k] + 64u * b;
-        quad_compress(cl, ch, ivq, dq, ab);
+        // the next block's round-0 words (this block's again after the last)
+        const uint32_t nb_off = uint32_t(b) + 1 < nb ? 64u * (b + 1) : 64u * b;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nxt[k] = addr[k] + nb_off;
+        quad_compress_m<true>(cl, ch, ivq, dq, ab, m, nxt);
       }
     }
   }
@@ -1844,7 +1939,7 @@ __device__ __forceinline__ void one_stage(uint4 *img_u4, const uint8_t *src, uin
         for (uint32_t k = 0; p + k < have; ++k) w[k >> 2] |= uint32_t(src[p + k]) << (8 * (k & 3));
         v[i] = make_uint4(w[0], w[1], w[2], w[3]);
       }
-      img_u4[p >> 4] = v[i];
+      img_u4[img_g(p >> 4)] = v[i];
       if (dcopy) *reinterpret_cast<uint4 *>(dcopy + p) = v[i];
     }
   }
@@ -1864,12 +1959,12 @@ __device__ __forceinline__ void one_xor(uint4 *img_u4, uint32_t len, const uint3
     if (avail < 64) mask_tail(x, avail);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      uint4 v = img_u4[kb * 4 + i];
+      uint4 v = img_u4[img_g(kb * 4 + i)];
       v.x ^= x[4 * i];
       v.y ^= x[4 * i + 1];
       v.z ^= x[4 * i + 2];
       v.w ^= x[4 * i + 3];
-      img_u4[kb * 4 + i] = v;
+      img_u4[img_g(kb * 4 + i)] = v;
     }
   }
 }
@@ -1878,7 +1973,7 @@ __device__ __forceinline__ void one_xor(uint4 *img_u4, uint32_t len, const uint3
 template <int LANES>
 __device__ __forceinline__ void one_store(const uint4 *img_u4, uint8_t *dst, uint32_t len) {
   for (uint32_t p = threadIdx.x * 16u; p < len; p += LANES * 16u) {
-    const uint4 v = img_u4[p >> 4];
+    const uint4 v = img_u4[img_g(p >> 4)];
     if (p + 16u <= len) {
       *reinterpret_cast<uint4 *>(dst + p) = v;
     } else {
@@ -2099,7 +2194,7 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint32_t p = (tid + uint32_t(i) * 256u) * 16u;
-      if (p < padded) img_u4[p >> 4] = v[i];
+      if (p < padded) img_u4[img_g(p >> 4)] = v[i];
     }
   }
   uint32_t dek[8];
@@ -3103,6 +3198,7 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
 // The fine-item share of k_pass_dc's CID items: the last ceil(m / 4)
 // messages of each work list.
 constexpr uint32_t kDcFineDiv = 4;
+
 
 // Split-mode post of many-wave size in one launch (k_pass_dc): both passes
 // of launch_keyed_hash + launch_cid_pass when each would be one k_pass<G,
