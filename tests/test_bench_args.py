@@ -51,3 +51,28 @@ def test_bench_exits_nonzero_without_enough_gpus():
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
     assert "bench.py:" in p.stderr and not p.stdout.strip()
+
+
+def test_cpu_baseline_cores_are_labelled(monkeypatch):
+    """the CPU baselines' thread count is the job's core
+    share (job_cores), never more than the affinity mask allows, and the
+    line records what it ran on (affinity size, OMP_NUM_THREADS, nproc)."""
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.job_cores() == min(3, aff)
+    monkeypatch.setenv("OMP_NUM_THREADS", str(aff + 100))
+    assert bench.job_cores() == aff
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.job_cores() == aff
+    info = bench.core_info()
+    assert set(info) == {"job_cores", "sched_affinity", "OMP_NUM_THREADS", "nproc"}
+    assert info["sched_affinity"] == aff and info["nproc"] == os.cpu_count()
+
+
+def test_fused_reruns_fail_the_run():
+    """the bench line reports re-runs of failed one-launch
+    split posts per timed leg and a non-zero count fails the run."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('out["fused_reruns"] = reruns') == 2     # both modes
+    assert src.count("glfsx_fused_failures()") >= 6
+    assert src.count("sys.exit(3)") == 2
