@@ -23,6 +23,8 @@ def main():
     bs = int(sys.argv[2]) if len(sys.argv) > 2 else 2 << 20
     size = int(gib * (1 << 30))
     N.set_device(0)
+    if os.environ.get("WG_LATENCY"):  # pass_plan's latency bound (glfsx_set_latency_wgs)
+        N.lib.glfsx_set_latency_wgs(int(os.environ["WG_LATENCY"]))
     fn = N.lib.glfsx_debug_wgtime
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p]
