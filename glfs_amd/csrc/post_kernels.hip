@@ -2679,6 +2679,15 @@ hipError_t launch_g(const KArgs &a, bool aligned, hipStream_t s) {
 std::atomic<uint32_t> g_split_target{2048u};
 constexpr uint32_t kMaxSplitLog2 = 8;  // the last workgroup merges <= 256 CVs
 constexpr uint64_t kDcMinWgs = 1024;   // see pass_plan
+// A/B switches (tools/build_variant.sh): GLFSX_LAT_ADJ=0 keeps pass_plan's
+// plan for 320-1023 workgroups instead of moving it to the latency form;
+// GLFSX_DC=0 never runs the one-launch split post (k_pass_dc)
+#ifndef GLFSX_LAT_ADJ
+#define GLFSX_LAT_ADJ 1
+#endif
+#ifndef GLFSX_DC
+#define GLFSX_DC 1
+#endif
 
 // Split-mode scratch (32 B per workgroup) and arrival counters (4 B per
 // message, zero between launches: each message's last workgroup resets its
@@ -2898,7 +2907,7 @@ void pass_plan(uint64_t n, uint64_t maxlen, int *g_out, uint32_t *sl_out) {
   // 1 MiB and up, keep the one-launch plan (scripts/r4_plan_sweep.py,
   // DESIGN.md section 5)
   const uint64_t lat = uint64_t(g_latency_wgs.load(std::memory_order_relaxed)) * 5 / 8;
-  if (sl > 0 && g <= 4 && (n << sl) > lat && (n << sl) < kDcMinWgs) {
+  if (GLFSX_LAT_ADJ && sl > 0 && g <= 4 && (n << sl) > lat && (n << sl) < kDcMinWgs) {
     int bg = 0;
     uint32_t bsl = 0;
     for (int gg = g0, s = int(sl0); gg >= 1 && s <= int(kMaxSplitLog2); gg /= 2, ++s)
@@ -3205,7 +3214,7 @@ constexpr uint32_t kDcFineDiv = 4;
 // CHACHA, true, 2> launch with the same plan.
 hipError_t launch_post_fused(const PostJob &job, hipStream_t s, bool *done) {
   *done = false;
-  if (job.n < 2 || !is_aligned(job)) return hipSuccess;
+  if (!GLFSX_DC || job.n < 2 || !is_aligned(job)) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(job.out.refs) | job.out.stride) & 3) return hipSuccess;
   const uint64_t maxlen = std::max(job.msg_len, job.last_len);
   int g;
