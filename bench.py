@@ -1186,10 +1186,13 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
             best = dt if best is None else min(best, dt)
         return round(n / GIB / best, 2)
 
-    def read_from(piece):
+    def read_from(piece, strict=False):
         """io.Copy through the Writer's ReadFrom (glfsx_writer_reserve /
         _commit): a reader that copies up to `piece` bytes per Read straight
-        into the pinned staging (one thread, like read(2) from a file)."""
+        into the pinned staging (one thread, like read(2) from a file).
+        strict: the Go binding's default writer (GLFSX_STRICT=1), whose
+        ReadFrom turns strict off for its batches, then back on and flushes
+        before returning (integration/go/gpu.go ReadFrom)."""
         best = None
         buf, cap = ctypes.c_void_p(), ctypes.c_uint64()
         for _ in range(3):
@@ -1200,6 +1203,9 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
             w = N.lib.glfsx_writer_new(bs, bs, None, None, store_post, c, ctypes.byref(err))
             assert w, N.last_error()
             off, rc = 0, 0
+            if strict:
+                N.check(N.lib.glfsx_writer_set_strict(w, 1))
+                N.check(N.lib.glfsx_writer_set_strict(w, 0))   # ReadFrom's entry
             while rc == 0 and off < n:
                 rc = N.lib.glfsx_writer_reserve(w, ctypes.byref(buf), ctypes.byref(cap))
                 if rc == 0:
@@ -1207,6 +1213,9 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                     ctypes.memmove(buf.value, host.ctypes.data + off, k)
                     rc = N.lib.glfsx_writer_commit(w, k)
                     off += k
+            if rc == 0 and strict:   # ReadFrom's return
+                N.check(N.lib.glfsx_writer_set_strict(w, 1))
+                rc = N.lib.glfsx_writer_flush(w)
             if rc == 0:
                 rc = N.lib.glfsx_writer_finish(w, ctypes.byref(root))
             msg = (N.lib.glfsx_writer_error(w) or b"").decode()
@@ -1221,6 +1230,7 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
     res["io_copy_32k_strict"] = io_copy(True, 32 << 10)
     res["read_from_1m"] = read_from(MIB)
     res["read_from_64m"] = read_from(64 * MIB)
+    res["read_from_1m_strict"] = read_from(MIB, strict=True)
     while stores:
         N.lib.glfsx_store_free(stores.pop())
     home = int(torch.cuda.current_device())
@@ -1252,6 +1262,9 @@ def host_round_trip(N, args, bs, barrier=lambda: None, slowest=lambda s: s):
                                 "/_commit): the reader copies 1 MiB per Read straight into "
                                 "the pinned staging (one thread, no second copy)",
                 "read_from_64m": "the same with 64 MiB Reads",
+                "read_from_1m_strict": "read_from_1m on a strict writer, the Go binding's "
+                                       "default (GLFSX_STRICT=1): ReadFrom pipelines its "
+                                       "batches and flushes their Posts before returning",
                 "file_read_fd": ff["what"] + " (one lane)",
                 "file_read_fd_3_lanes": "the same, the Writer's batches over 3 lanes of the "
                                         "one GPU ([0, 0, 0]: shared streams, more slots in "

@@ -130,6 +130,7 @@ class Writer:
                                          ctypes.byref(err))
         if not self._w:
             N.check(err.value)
+        self._strict = bool(strict)
         if strict:
             # blob.go:120-133 error timing: every Write returns after the
             # Posts of the blocks it completed were delivered
@@ -200,7 +201,24 @@ class Writer:
         position to its end by several threads at once straight into the
         writer's pinned staging (glfsx_writer_read_fd), then positioned after
         what was read; any other stream goes r.readinto() straight into the
-        staging (glfsx_writer_reserve / glfsx_writer_commit), no second copy."""
+        staging (glfsx_writer_reserve / glfsx_writer_commit), no second copy.
+        Strict writer (the Go binding's default, integration/go/gpu.go
+        ReadFrom): the call's batches are pipelined and their Posts delivered
+        before it returns, so a store error comes back from this call -- where
+        the reference's io.Copy returns it -- after the same Posts."""
+        if not self._strict:
+            return self._read_from(r)
+        N.check(N.lib.glfsx_writer_set_strict(self._w, 0))
+        try:
+            got = self._read_from(r)
+        finally:
+            N.check(N.lib.glfsx_writer_set_strict(self._w, 1))
+            rc = N.lib.glfsx_writer_flush(self._w)
+            if rc:
+                self._raise(rc)   # a store error before the reader's own
+        return got
+
+    def _read_from(self, r) -> int:
         fd = _regular_fd(r)
         if fd is not None:
             pos = r.tell()

@@ -8,12 +8,14 @@
 // CGO_LDFLAGS="-L<glfsx>/lib -lglfsx" go build -tags glfsgpu ./...
 //
 // Environment:
-//   GLFSX_STRICT=1   blob.go:120-133 error timing (a store error comes back
-//                    from the Write that completed the failing block); the
-//                    default 0 pipelines 64 MiB batches and returns it from
-//                    the Write or Finish whose batch held it -- the Posts
-//                    are the same prefix either way, and Create returns the
-//                    same error.
+//   GLFSX_STRICT=1   (the default) blob.go:120-133 error timing: a store
+//                    error comes back from the Write that completed the
+//                    failing block, and from the ReadFrom (io.Copy) call
+//                    that fed it -- ReadFrom pipelines its own batches and
+//                    delivers their Posts before it returns.  0 pipelines
+//                    Write too: the error comes from the Write or Finish
+//                    whose 64 MiB batch held it (the Posts are the same
+//                    prefix either way, and Create returns the same error).
 //   GLFSX_DEVICES=0,1,...  hash each Writer's batches round-robin on these
 //                    GPUs (one Writer fed by one io.Reader over several PCIe
 //                    links; Posts still in block order).
@@ -108,7 +110,7 @@ type PrehashedWO interface {
 
 var (
 	parityEvery = envInt("GLFSX_PARITY", 0)
-	strict      = envInt("GLFSX_STRICT", 0)
+	strict      = envInt("GLFSX_STRICT", 1)
 	devices     = envInts("GLFSX_DEVICES")
 	// A blob shorter than this (and than one block) never reaches the GPU:
 	// the reference's own Go path posts it.  One PostBlob per small file
@@ -341,7 +343,27 @@ var fdRouteReads uint64
 // gpuDeviceCount is glfsx_device_count for the tests (no cgo in _test.go).
 func gpuDeviceCount() int { return int(C.glfsx_device_count()) }
 
-// ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341).
+// ReadFrom is io.Copy's fast path (Create, Concat: blob.go:213,341).  In
+// strict mode (the default) the reference's io.Copy returns a store error
+// from the Write that completed the failing block, i.e. from this call: the
+// batches this call feeds are pipelined (the writer's strict flag is off
+// meanwhile, so a generic reader's commits do not wait one block at a time)
+// and glfsx_writer_flush delivers their Posts before it returns, so the
+// error still comes back from this call, with the same Posts before it.
+func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
+	if strict == 0 {
+		return gw.readFromRoutes(r)
+	}
+	C.glfsx_writer_set_strict(gw.w, 0)
+	n, err := gw.readFromRoutes(r)
+	C.glfsx_writer_set_strict(gw.w, 1)
+	if rc := C.glfsx_writer_flush(gw.w); rc != 0 {
+		return n, gw.fail(rc) // a store error before the reader's own
+	}
+	return n, err
+}
+
+// readFromRoutes feeds the writer from r:
 //   - A regular file (an *os.File, or io.Copy's fileWithoutWriteTo wrapper
 //     of one; plainFile): read from its current offset to its end by the
 //     library's reader threads with pread(2), straight into the writer's
@@ -355,7 +377,7 @@ func gpuDeviceCount() int { return int(C.glfsx_device_count()) }
 //     once, by r.Read, instead of into io.Copy's 32 KiB buffer and again by
 //     Write.  C memory handed to Go as a slice is fine under the cgo rules;
 //     it is not used after commit.
-func (gw *gpuWriter) ReadFrom(r io.Reader) (int64, error) {
+func (gw *gpuWriter) readFromRoutes(r io.Reader) (int64, error) {
 	if f, ok := plainFile(r); ok {
 		if st, err := f.Stat(); err == nil && st.Mode().IsRegular() {
 			if pos, err := f.Seek(0, io.SeekCurrent); err == nil {

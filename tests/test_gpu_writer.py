@@ -108,6 +108,40 @@ def test_default_error_no_posts_after_failure(gpu, O):
     assert [(k, r) for k, r, _ in st.inner.log] == want_posts
 
 
+@pytest.mark.parametrize("fail_at", [1, 17, 35, 41, 43])
+def test_strict_read_from_returns_the_io_copy_error(gpu, O, fail_at):
+    """The Go binding's default (GLFSX_STRICT=1) ReadFrom: pipelined inside
+    the call, its Posts flushed before it returns.  The reference's io.Copy
+    (32 KiB Writes, blob.go:120-133) returns a store error from the copy when
+    the failing Post belongs to a block the input completed, else Finish
+    does; the GPU writer's read_from / finish must fail at the same place,
+    after exactly the same Posts."""
+    import io
+    from glfs_amd import bigblob
+    bs = 1024                       # bf = 16: index posts interleave
+    data = O.fill_splitmix(40 * bs + 300, 29)
+    pieces = [32768] * (len(data) // 32768) + [len(data) % 32768]
+    want_at, want_posts = _oracle_fail_run(O, data, bs, pieces, fail_at)
+    want = None if want_at is None else ("finish" if want_at == "finish" else "copy")
+    st = _FailingStore(bs, fail_at)
+    w = bigblob.Machine(bs).new_writer(st, None, strict=True)
+    got = None
+    try:
+        try:
+            assert w.read_from(io.BytesIO(data)) == len(data)
+        except bigblob.StoreError:
+            got = "copy"
+        if got is None:
+            try:
+                w.finish()
+            except bigblob.StoreError:
+                got = "finish"
+    finally:
+        w.close()
+    assert got == want
+    assert [(k, r) for k, r, _ in st.inner.log] == want_posts
+
+
 def test_flush_delivers_complete_blocks(gpu, O):
     from glfs_amd import bigblob
     bs = 1 << 20

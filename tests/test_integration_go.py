@@ -197,7 +197,7 @@ def test_read_from_matches_io_copy_file_wrapper():
     and must NOT match, so nothing is matched by method set.  gpu_test.go
     (glfsgpu tag) checks both through io.Copy."""
     src = _read("gpu.go")
-    body = src[src.index("func (gw *gpuWriter) ReadFrom("):]
+    body = src[src.index("func (gw *gpuWriter) readFromRoutes("):]
     body = body[:body.index("\n}\n")]
     assert "r.(osFile)" not in body and "plainFile(r)" in body
     assert "positionedReader(r)" in body and "io.ReaderAt\n" not in body
@@ -217,3 +217,21 @@ def test_read_from_matches_io_copy_file_wrapper():
     assert "type upperFile struct{ *os.File }" in test
     assert "TestCreateFromFileWrapperUsesItsRead" in test
     assert test.count("{") == test.count("}") and test.count("(") == test.count(")")
+
+
+def test_strict_error_timing_is_the_default():
+    """the drop-in returns a store error where the
+    reference does by default (GLFSX_STRICT=1): Write with blob.go:120-133's
+    timing; ReadFrom pipelines its own batches with the writer's strict flag
+    off and flushes before it returns, so io.Copy still gets the error
+    (tests/test_gpu_writer.py::test_strict_read_from_returns_the_io_copy_error
+    runs the same sequence through the C-ABI)."""
+    src = _read("gpu.go")
+    assert 'strict      = envInt("GLFSX_STRICT", 1)' in src
+    body = src[src.index("func (gw *gpuWriter) ReadFrom("):]
+    body = body[:body.index("\n}\n")]
+    assert "C.glfsx_writer_set_strict(gw.w, 0)" in body
+    assert body.index("C.glfsx_writer_set_strict(gw.w, 0)") < body.index("n, err := gw.readFromRoutes(r)") \
+        < body.index("C.glfsx_writer_set_strict(gw.w, 1)") < body.index("C.glfsx_writer_flush(gw.w)")
+    assert "func (gw *gpuWriter) readFromRoutes(r io.Reader) (int64, error) {" in src
+    assert src.count("{") == src.count("}") and src.count("(") == src.count(")")
