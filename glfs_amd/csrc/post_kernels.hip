@@ -3206,7 +3206,10 @@ hipError_t launch_keyed_hash(const PostJob &job, uint32_t out_off,
 
 // The fine-item share of k_pass_dc's CID items: the last ceil(m / 4)
 // messages of each work list.
-constexpr uint32_t kDcFineDiv = 4;
+#ifndef GLFSX_DC_FINE_DIV  // A/B switch (tools/build_variant.sh); 0: no fine items
+#define GLFSX_DC_FINE_DIV 4
+#endif
+constexpr uint32_t kDcFineDiv = GLFSX_DC_FINE_DIV;
 
 
 // Split-mode post of many-wave size in one launch (k_pass_dc): both passes
