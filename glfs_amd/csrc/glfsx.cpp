@@ -32,6 +32,13 @@
 
 using namespace glfsx;
 
+// A/B switch (tools/build_variant.sh): a launch of one one-shot post (of
+// either size class) passes its descriptor by value (launch_one_v /
+// launch_med_v) instead of through the pinned descriptor array.
+#ifndef GLFSX_ONE_BYVAL
+#define GLFSX_ONE_BYVAL 1
+#endif
+
 namespace {
 
 thread_local std::string tls_err;
@@ -390,8 +397,14 @@ int one_launch(OneLane &L, const std::vector<OneReq *> &batch, uint32_t seq) {
     mo += (d.len + 255) & ~uint64_t(255);
     L.h_desc[im++] = d;
   }
-  if (ns) HIP_TRY(launch_one(L.d_desc, uint32_t(ns), max_small, L.s));
-  if (nm) HIP_TRY(launch_med(L.d_desc + ns, uint32_t(nm), max_med, L.s));
+  if (ns == 1 && GLFSX_ONE_BYVAL)
+    HIP_TRY(launch_one_v(L.h_desc[0], L.s));
+  else if (ns)
+    HIP_TRY(launch_one(L.d_desc, uint32_t(ns), max_small, L.s));
+  if (nm == 1 && GLFSX_ONE_BYVAL)
+    HIP_TRY(launch_med_v(L.h_desc[ns], L.s));
+  else if (nm)
+    HIP_TRY(launch_med(L.d_desc + ns, uint32_t(nm), max_med, L.s));
   HIP_TRY(hipEventRecord(L.ev, L.s));
   return 0;
 }

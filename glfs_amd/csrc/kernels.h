@@ -135,6 +135,10 @@ hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
                       hipStream_t s);
 hipError_t launch_med(const OneDesc *descs, uint32_t n, uint64_t max_len,
                       hipStream_t s);
+// One post, its descriptor passed by value: d.len <= kMaxOneLen (launch_one_v)
+// or kMaxOneLen < d.len <= kMaxMedLen (launch_med_v).
+hipError_t launch_one_v(const OneDesc &d, hipStream_t s);
+hipError_t launch_med_v(const OneDesc &d, hipStream_t s);
 
 // Read side: decrypt n contiguous blocks (bs % 64 == 0; the last one
 // last_len bytes) with the DEKs in bytes [32,64) of refs[j] (dense).

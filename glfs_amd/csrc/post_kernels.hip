@@ -2032,8 +2032,11 @@ __device__ unsigned long long g_one_t[16];
   } while (0)
 #endif
 
-template <int QUADS>
-__global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
+// The body of a one-shot post (k_one, k_one_v).  V: dp is the descriptor
+// itself (a kernel argument); otherwise the launch's array in pinned host
+// memory, staged by one_desc.
+template <int QUADS, bool V>
+__device__ __forceinline__ void one_run(const OneDesc *g) {
 #if GLFSX_ONE_TIMING
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2041,9 +2044,14 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
   __shared__ uint4 ts_u4[QUADS / 2 * 4];     // parent inputs of the merge
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_dek[8];
-  __shared__ OneDesc s_desc;
   constexpr int kLanes = QUADS * 4;
-  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x);
+  const OneDesc *dp;
+  if constexpr (V) {
+    dp = g;
+  } else {
+    __shared__ OneDesc s_desc;
+    dp = one_desc(&s_desc, g + blockIdx.x);
+  }
   const uint32_t len = dp->len;
   const uint32_t tid = threadIdx.x, q = tid & 3u, quad = tid >> 2;
   const uint32_t img = lds_offset(img_u4), ts = lds_offset(ts_u4);
@@ -2097,6 +2105,20 @@ __global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
 #endif
 }
 
+template <int QUADS>
+__global__ __launch_bounds__(QUADS * 4) void k_one(const OneDesc *descs) {
+  one_run<QUADS, false>(descs);
+}
+
+// A launch of one post (the common case of a caller posting alone): the
+// descriptor travels as the kernel argument, so its fields are read from the
+// kernarg segment instead of one PCIe round trip to pinned host memory ahead
+// of everything else (round 6).
+template <int QUADS>
+__global__ __launch_bounds__(QUADS * 4) void k_one_v(const OneDesc d) {
+  one_run<QUADS, true>(&d);
+}
+
 // ---- Medium one-shot posts (kMaxOneLen < len <= kMaxMedLen) ----
 // Workgroup s of a message owns its 64 KiB span s (64 chunks, one per quad).
 // k_med_dek stages the span from the caller's staging (pinned host memory)
@@ -2132,13 +2154,21 @@ __device__ __forceinline__ void med_publish_merge(uint32_t &cl, uint32_t &ch, co
   if (tid == 0) *dp->cnt = 0;
 }
 
-__global__ __launch_bounds__(256) void k_med_dek(const OneDesc *descs, uint32_t wmax) {
+// V: g is the descriptor itself (a kernel argument, one message); else the
+// launch's array (as one_run)
+template <bool V>
+__device__ __forceinline__ void med_dek_run(const OneDesc *g, uint32_t wmax) {
   __shared__ uint4 img_u4[64 * 64];
   __shared__ uint4 ts_u4[32 * 4];
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_flag;
-  __shared__ OneDesc s_desc;
-  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x / wmax);
+  const OneDesc *dp;
+  if constexpr (V) {
+    dp = g;
+  } else {
+    __shared__ OneDesc s_desc;
+    dp = one_desc(&s_desc, g + blockIdx.x / wmax);
+  }
   const uint32_t sidx = blockIdx.x % wmax;
   const uint32_t len = dp->len;
   const uint32_t W = (len + 65535u) >> 16;
@@ -2168,13 +2198,19 @@ __global__ __launch_bounds__(256) void k_med_dek(const OneDesc *descs, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t wmax) {
+template <bool V>
+__device__ __forceinline__ void med_cid_run(const OneDesc *g, uint32_t wmax) {
   __shared__ uint4 img_u4[64 * 64];
   __shared__ uint4 ts_u4[32 * 4];
   __shared__ uint32_t passbuf[8];
   __shared__ uint32_t s_flag;
-  __shared__ OneDesc s_desc;
-  const OneDesc *dp = one_desc(&s_desc, descs + blockIdx.x / wmax);
+  const OneDesc *dp;
+  if constexpr (V) {
+    dp = g;
+  } else {
+    __shared__ OneDesc s_desc;
+    dp = one_desc(&s_desc, g + blockIdx.x / wmax);
+  }
   const uint32_t sidx = blockIdx.x % wmax;
   const uint32_t len = dp->len;
   const uint32_t W = (len + 65535u) >> 16;
@@ -2185,10 +2221,14 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
   // the device copy holds the span zero padded to 64 B (k_med_dek)
   const uint32_t padded = (slen + 63) & ~63u;
   {
-    uint4 v[16];  // all loads in flight at once (see one_stage)
+    // all loads in flight at once (see one_stage).  Zero-initialised: left
+    // partly unassigned, the array stayed in scratch -- each load waited for
+    // and spilled before the next was issued (the code object of rounds 5-6)
+    uint4 v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint32_t p = (tid + uint32_t(i) * 256u) * 16u;
+      v[i] = make_uint4(0, 0, 0, 0);
       if (p < padded) v[i] = *reinterpret_cast<const uint4 *>(dp->dmsg + off + p);
     }
 #pragma unroll
@@ -2229,6 +2269,20 @@ __global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t 
     r[4 + q] = ch;
   }
   if (last) one_signal(dp);
+}
+
+__global__ __launch_bounds__(256) void k_med_dek(const OneDesc *descs, uint32_t wmax) {
+  med_dek_run<false>(descs, wmax);
+}
+__global__ __launch_bounds__(256) void k_med_cid(const OneDesc *descs, uint32_t wmax) {
+  med_cid_run<false>(descs, wmax);
+}
+// One medium post, its descriptor as the kernel argument (k_one_v)
+__global__ __launch_bounds__(256) void k_med_dek_v(const OneDesc d, uint32_t wmax) {
+  med_dek_run<true>(&d, wmax);
+}
+__global__ __launch_bounds__(256) void k_med_cid_v(const OneDesc d, uint32_t wmax) {
+  med_cid_run<true>(&d, wmax);
 }
 
 // Small blobs (glfs.PostBlob of many blobs that each fit one bigblob block,
@@ -3420,6 +3474,25 @@ hipError_t launch_one(const OneDesc *descs, uint32_t n, uint64_t max_len,
     hipLaunchKernelGGL(k_one<16>, dim3(n), dim3(64), 0, s, descs);
   else
     hipLaunchKernelGGL(k_one<64>, dim3(n), dim3(256), 0, s, descs);
+  return hipGetLastError();
+}
+
+hipError_t launch_med_v(const OneDesc &d, hipStream_t s) {
+  if (d.len > kMaxMedLen || d.len <= kMaxOneLen) return hipErrorInvalidValue;
+  const uint32_t wmax = uint32_t((uint64_t(d.len) + 65535) >> 16);
+  hipLaunchKernelGGL(k_med_dek_v, dim3(wmax), dim3(256), 0, s, d, wmax);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_med_cid_v, dim3(wmax), dim3(256), 0, s, d, wmax);
+  return hipGetLastError();
+}
+
+hipError_t launch_one_v(const OneDesc &d, hipStream_t s) {
+  if (d.len > kMaxOneLen) return hipErrorInvalidValue;
+  if (d.len <= 16 * 1024)
+    hipLaunchKernelGGL(k_one_v<16>, dim3(1), dim3(64), 0, s, d);
+  else
+    hipLaunchKernelGGL(k_one_v<64>, dim3(1), dim3(256), 0, s, d);
   return hipGetLastError();
 }
 
