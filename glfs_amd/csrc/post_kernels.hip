@@ -2065,7 +2065,19 @@ __device__ __forceinline__ void one_run(const OneDesc *g) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) key[i] = dp->salt[i];
   uint32_t cl, ch;
+#if GLFSX_ONE_TIMING  // one_hash with a stamp between its chunks and its merges
+  {
+    const uint32_t kq_lo = qsel(q, key[0], key[1], key[2], key[3]);
+    const uint32_t kq_hi = qsel(q, key[4], key[5], key[6], key[7]);
+    const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+    one_chunks(cl, ch, img, len, 0u, true, kq_lo, kq_hi, ivq, kKeyed, q, quad, rel);
+    ONE_T(6);
+    one_tree(cl, ch, len ? (len + 1023) >> 10 : 1u, true, ts, passbuf, kq_lo, kq_hi, ivq,
+             kKeyed, q, quad, rel);
+  }
+#else
   one_hash(cl, ch, img, ts, passbuf, len, key, kKeyed, q, quad, rel);
+#endif
   if (quad == 0) {  // lanes 0-3: DEK words q and 4+q
     s_dek[q] = cl;
     s_dek[4 + q] = ch;
@@ -2082,7 +2094,20 @@ __device__ __forceinline__ void one_run(const OneDesc *g) {
   uint32_t ckey[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ckey[i] = dp->cid_key[i];
+#if GLFSX_ONE_TIMING
+  {
+    const uint32_t cb = dp->cid_keyed ? kKeyed : 0u;
+    const uint32_t kq_lo = qsel(q, ckey[0], ckey[1], ckey[2], ckey[3]);
+    const uint32_t kq_hi = qsel(q, ckey[4], ckey[5], ckey[6], ckey[7]);
+    const uint32_t ivq = qsel(q, kIV[0], kIV[1], kIV[2], kIV[3]);
+    one_chunks(cl, ch, img, len, 0u, true, kq_lo, kq_hi, ivq, cb, q, quad, rel);
+    ONE_T(7);
+    one_tree(cl, ch, len ? (len + 1023) >> 10 : 1u, true, ts, passbuf, kq_lo, kq_hi, ivq, cb,
+             q, quad, rel);
+  }
+#else
   one_hash(cl, ch, img, ts, passbuf, len, ckey, dp->cid_keyed ? kKeyed : 0u, q, quad, rel);
+#endif
   if (quad == 0) {
     uint32_t *r = reinterpret_cast<uint32_t *>(dp->ref);
     r[q] = cl;

@@ -43,8 +43,9 @@ def run(size, calls=400):
         timing(0, tv)
         k = max(tv[15], 1)
         out["k_one_phase_end_us"] = dict(zip(
-            ("read_desc", "stage", "dek", "keystream", "cid_ref", "signal"),
-            (round(tv[i] / k / 100.0, 2) for i in range(6))))   # 100 MHz ticks
+            ("read_desc", "stage", "dek", "keystream", "cid_ref", "signal",
+             "dek_chunks", "cid_chunks"),
+            (round(tv[i] / k / 100.0, 2) for i in range(8))))   # 100 MHz ticks
         out["timed_launches"] = tv[15]
         out["k_one_clock_GHz"] = round(tv[13] / max(tv[14], 1) * 0.1, 3)
     print(json.dumps(out))
