@@ -1432,6 +1432,58 @@ __device__ __forceinline__ uint32_t qrot3(uint32_t x) {  // lane q <- lane q+3
 #define GLFSX_QASM 1
 #endif
 
+// Every row rotation folded into its first consumer (v_add_u32_dpp /
+// v_xor_b32_dpp, the permute on src0): b, c, d stay in the diagonal frame
+// (lanes q+1, q+2, q+3) from a diagonal step until the next column step
+// reads them back; a never moves.  26 ARX instructions, one filler add and
+// two s_nop 0 per round (a DPP read of a VGPR written one or two
+// instructions before needs two wait states) against QROUND_ASM's 33.
+// In: t = a + m0; the state in the column frame (QCOL0) or the diagonal
+// frame (QCOL).  Out: the diagonal frame.  tools/qchain.hip v4: 1118 vs
+// 1233 cycles per compression at one wave per SIMD; PostBlob 4 KiB p50
+// 40.4 -> 37.7 us, config 2's index-node kernels 62.8 -> 57.9 us
+// (scripts/ab_qfold.sh, profiles/r6/ab_qfold/).  GLFSX_QFOLD=0 (A/B builds):
+// QROUND_ASM.
+#ifndef GLFSX_QFOLD
+#define GLFSX_QFOLD 1
+#endif
+#define QCOL0_ASM                                                               \
+  "v_add_u32 %0, %1, %4\n"                                                      \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 12\n"
+#define QCOL_ASM                                                                \
+  "s_nop 0\n"                                                                   \
+  "v_add_u32_dpp %0, %1, %4 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %3, %3, %0 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32_dpp %2, %2, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %1, %1, %2 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %1, %1, %1, 12\n"
+#define QREST_ASM                                                               \
+  "v_add3_u32 %0, %0, %1, %5\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 7\n"                                              \
+  "v_add_u32 %4, %0, %6\n"                                                      \
+  "s_nop 0\n"                                                                   \
+  "v_add_u32_dpp %0, %1, %4 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %3, %3, %0 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32_dpp %2, %2, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %1, %1, %2 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %1, %1, %1, 12\n"                                             \
+  "v_add3_u32 %0, %0, %1, %7\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 7\n"
+
 // One compression in quad layout.  addr[4r+k]: LDS byte address of the k-th
 // message word this lane uses in round r.  On return (a, b) = (cv[q], cv[4+q]).
 // Every lane of a quad must be active (the rotations read the other three).
@@ -1455,13 +1507,29 @@ __device__ __forceinline__ void quad_compress_m(uint32_t &a, uint32_t &b, uint32
       for (int k = 0; k < 4; ++k) n[k] = *reinterpret_cast<lds_word>(nxt[k]);
     }
     uint32_t t = a + m[0];
-    asm volatile(QROUND_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
-                 : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+    if (!GLFSX_QFOLD)
+      asm volatile(QROUND_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                   : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+    else if (r == 0)
+      asm volatile(QCOL0_ASM QREST_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                   : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+    else
+      asm volatile(QCOL_ASM QREST_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                   : "v"(m[1]), "v"(m[2]), "v"(m[3]));
 #pragma unroll
     for (int k = 0; k < 4; ++k) m[k] = n[k];
   }
-  a ^= c;
-  b ^= d;
+  if (!GLFSX_QFOLD) {
+    a ^= c;
+    b ^= d;
+  } else {  // back from the diagonal frame: a ^= c_q, b = b_q ^ d_q
+    uint32_t u;
+    asm volatile("v_xor_b32_dpp %0, %2, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+                 "s_nop 1\n"
+                 "v_mov_b32_dpp %4, %1 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"
+                 "v_xor_b32_dpp %1, %3, %4 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&v"(u));
+  }
 }
 
 __device__ __forceinline__ void quad_compress(uint32_t &a, uint32_t &b,

@@ -203,6 +203,78 @@ __device__ __forceinline__ void qc_v3(uint32_t &a, uint32_t &b, uint32_t c, uint
   b ^= d;
 }
 
+// v4: every row rotation folded into its first consumer (v_add_u32_dpp /
+// v_xor_b32_dpp, DPP on src0), the state left in the diagonal frame between
+// steps: b, c, d go to lanes q+1, q+2, q+3 for the diagonal step and back
+// in the next column step; a never moves.  Per round 26 ARX instructions,
+// one filler add and two s_nop 0 (a DPP read of a VGPR written by one of
+// the two instructions before it) instead of 33.
+#define QCOL0_ASM                                                               \
+  "v_add_u32 %0, %1, %4\n"                                                      \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 12\n"
+#define QCOL_ASM                                                                \
+  "s_nop 0\n"                                                                   \
+  "v_add_u32_dpp %0, %1, %4 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %3, %3, %0 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32_dpp %2, %2, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %1, %1, %2 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %1, %1, %1, 12\n"
+#define QREST_ASM                                                               \
+  "v_add3_u32 %0, %0, %1, %5\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 7\n"                                              \
+  "v_add_u32 %4, %0, %6\n"                                                      \
+  "s_nop 0\n"                                                                   \
+  "v_add_u32_dpp %0, %1, %4 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %3, %3, %0 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %3, %3, %3, 16\n"                                             \
+  "v_add_u32_dpp %2, %2, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"   \
+  "v_xor_b32_dpp %1, %1, %2 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"   \
+  "v_alignbit_b32 %1, %1, %1, 12\n"                                             \
+  "v_add3_u32 %0, %0, %1, %7\n"                                                 \
+  "v_xor_b32 %3, %3, %0\n"                                                      \
+  "v_alignbit_b32 %3, %3, %3, 8\n"                                              \
+  "v_add_u32 %2, %2, %3\n"                                                      \
+  "v_xor_b32 %1, %1, %2\n"                                                      \
+  "v_alignbit_b32 %1, %1, %1, 7\n"
+
+__device__ __forceinline__ void qc_v4(uint32_t &a, uint32_t &b, uint32_t c, uint32_t d,
+                                      const uint32_t (&addr)[28]) {
+  uint32_t m[4] = {ldsw(addr[0]), ldsw(addr[1]), ldsw(addr[2]), ldsw(addr[3])};
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    uint32_t n[4] = {0, 0, 0, 0};
+    if (r < 6) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) n[k] = ldsw(addr[4 * r + 4 + k]);
+    }
+    uint32_t t = a + m[0];
+    if (r == 0)
+      asm volatile(QCOL0_ASM QREST_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                   : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+    else
+      asm volatile(QCOL_ASM QREST_ASM : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                   : "v"(m[1]), "v"(m[2]), "v"(m[3]));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = n[k];
+  }
+  // back from the diagonal frame: a ^= c_q, b = b_q ^ d_q
+  uint32_t u;
+  asm volatile("v_xor_b32_dpp %0, %2, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+               "s_nop 1\n"
+               "v_mov_b32_dpp %4, %1 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"
+               "v_xor_b32_dpp %1, %3, %4 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+               : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&v"(u));
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void k_chain(const uint32_t *msg, uint32_t *out, uint32_t iters,
                                                unsigned long long *clk) {
@@ -236,6 +308,7 @@ __global__ __launch_bounds__(256) void k_chain(const uint32_t *msg, uint32_t *ou
     if constexpr (V == 1) qc_v1(cl, ch, ivq, dq, addr);
     if constexpr (V == 2) qc_v2(cl, ch, ivq, dq, addr);
     if constexpr (V == 3) qc_v3(cl, ch, ivq, dq, addr);
+    if constexpr (V == 4) qc_v4(cl, ch, ivq, dq, addr);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   out[(blockIdx.x * 256 + tid) * 2] = cl;
@@ -262,12 +335,12 @@ int main(int argc, char **argv) {
     h[i] = uint32_t(x);
   }
   CK(hipMemcpy(msg, h, sizeof h, hipMemcpyHostToDevice));
-  void (*ks[4])(const uint32_t *, uint32_t *, uint32_t, unsigned long long *) = {
-      k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>};
+  void (*ks[5])(const uint32_t *, uint32_t *, uint32_t, unsigned long long *) = {
+      k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<4>};
   uint32_t *ref = static_cast<uint32_t *>(malloc(size_t(grid) * 256 * 8));
   uint32_t *got = static_cast<uint32_t *>(malloc(size_t(grid) * 256 * 8));
   printf("{\"iters\": %u, \"grid\": %d, \"variants\": {", iters, grid);
-  for (int v = 0; v < 4; ++v) {
+  for (int v = 0; v < 5; ++v) {
     hipLaunchKernelGGL(ks[v], dim3(grid), dim3(256), 0, 0, msg, out, 4u, clk);
     CK(hipDeviceSynchronize());
     unsigned long long best = ~0ull;
